@@ -1,0 +1,149 @@
+/*
+ * mcpx.h — C ABI of the MI355X-native batched interior-point MCP solver.
+ *
+ * This is the drop-in boundary for the Newton-step hot path of
+ * MixedComplementarityProblems.jl (TianyuQ/MCP).  One call replaces, for a
+ * whole batch of parameter vectors θ, the host loop of
+ *
+ *     solve(::InteriorPoint, mcp::PrimalDualMCP, θ; x₀, y₀, s₀, tol,
+ *           max_inner_iters, max_outer_iters, tightening_rate,
+ *           loosening_rate, min_stepsize, verbose, linear_solve_algorithm)
+ *                                                  reference src/solver.jl:35-51
+ *
+ * i.e. the per-instance block src/solver.jl:53-121 (residual F! and Jacobian
+ * ∇F_z! callbacks of src/mcp.jl:82-120, the regularised Newton solve
+ * src/solver.jl:81-90, the fraction-to-the-boundary line search
+ * src/solver.jl:93-100,127-138, the update src/solver.jl:103-108 and the
+ * ϵ-continuation src/solver.jl:71-121).  The reference binds nothing over an
+ * FFI today (it is pure Julia); the `ccall` a maintainer would add is shown in
+ * INTEGRATION.md.
+ *
+ * Problem families (how F and ∇F are evaluated on device per instance):
+ *
+ *   MCPX_FAMILY_QP      the convex-QP family of
+ *                       benchmark/quadratic_program_benchmark.jl:7-90:
+ *                         G(x,y;θ) = M x − ϕ − Aᵀ y,  H(x,y;θ) = A x − b,
+ *                       θ = [vec(M); vec(A); b; ϕ] column-major
+ *                       (unpack_parameters, :77-90), p = n² + m n + m + n.
+ *   MCPX_FAMILY_AFFINE  general affine MCP (any G/H affine in (x,y)):
+ *                         G = P x + Q y + g,  H = R x + S y + h,
+ *                       θ = [vec(P); vec(Q); vec(R); vec(S); g; h]
+ *                       column-major, p = n² + 2 n m + m² + n + m.
+ *                       (The Python front-end traces user G/H callables —
+ *                       src/mcp.jl:27-52, :155-210 — into this layout.)
+ *
+ * Conventions: all arrays are instance-major (instance b's data is contiguous,
+ * stride `theta_ld` for θ); all buffers are caller-owned; the library keeps no
+ * pointer after returning.  Return value 0 = OK, < 0 = API misuse / HIP error
+ * (message via mcpx_last_error(), thread-local).  Numerical failure is never
+ * an error: it is status[b] = MCPX_STATUS_FAILED, as in src/solver.jl:84-100,
+ * 117-119, which never throws.
+ */
+#ifndef MCPX_H
+#define MCPX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCPX_VERSION 10000 /* 1.0.0 */
+
+/* error codes */
+#define MCPX_OK 0
+#define MCPX_EINVAL (-1)      /* argument check failed (reference: ArgumentError / @assert) */
+#define MCPX_EHIP (-2)        /* HIP runtime error */
+#define MCPX_ENODEV (-3)      /* no usable gfx950 device */
+#define MCPX_EUNSUPPORTED (-4) /* size outside what the compiled kernels cover */
+
+/* per-instance status (reference: :solved / :failed, src/solver.jl:69,86,98,118) */
+#define MCPX_STATUS_SOLVED 0
+#define MCPX_STATUS_FAILED 1
+
+#define MCPX_FAMILY_QP 0
+#define MCPX_FAMILY_AFFINE 1
+
+/* KKT dimension N = n + 2m handled by the register-resident kernels */
+#define MCPX_MAX_KKT_DIM 64
+/* largest max_inner_iters (ϵ-schedule table length) */
+#define MCPX_MAX_INNER_ITERS 128
+/* largest number of line-search trials (α = decayᵉ, e = 0..E) */
+#define MCPX_MAX_LS_TRIALS 64
+
+/* Solver keyword arguments, same names and defaults as src/solver.jl:42-50;
+ * tau and decay are the hard-coded defaults of
+ * fraction_to_the_boundary_linesearch (src/solver.jl:127). */
+typedef struct mcpx_params {
+  double tol;               /* 1e-4 */
+  double tightening_rate;   /* 0.1  */
+  double loosening_rate;    /* 0.5  */
+  double min_stepsize;      /* 1e-4 (the docstring's 1e-2 is stale, src/solver.jl:31 vs :48) */
+  double tau;               /* 0.995 */
+  double decay;             /* 0.5  */
+  int32_t max_inner_iters;  /* 20 */
+  int32_t max_outer_iters;  /* 50 */
+} mcpx_params;
+
+/* Batch descriptor. */
+typedef struct mcpx_desc {
+  int32_t family;   /* MCPX_FAMILY_* */
+  int32_t n;        /* unconstrained_dimension (src/mcp.jl:22) */
+  int32_t m;        /* constrained_dimension   (src/mcp.jl:23) */
+  int32_t pad_;
+  int64_t batch;    /* number of instances B */
+  int64_t theta_ld; /* doubles between consecutive instances' θ (>= mcpx_theta_dim) */
+} mcpx_desc;
+
+/* Outputs, one record per instance.  Required: x, y, s, kkt_error, eps,
+ * outer_iters, status (the NamedTuple of src/solver.jl:121).  Optional
+ * (NULL = not wanted): newton_iters (total Newton steps taken),
+ * active_mask (bit k of word b*W + k/64 set iff y_k > s_k at return, W = max(1, ⌈m/64⌉)),
+ * alpha_trace (per accepted Newton step two bytes (e_s, e_y): α = decay^e;
+ * at most trace_len steps recorded per instance). */
+typedef struct mcpx_out {
+  double* x;            /* [B*n] */
+  double* y;            /* [B*m] */
+  double* s;            /* [B*m] */
+  double* kkt_error;    /* [B] */
+  double* eps;          /* [B] */
+  int32_t* outer_iters; /* [B] */
+  int32_t* status;      /* [B] */
+  int32_t* newton_iters;  /* [B] or NULL */
+  uint64_t* active_mask;  /* [B*W] or NULL */
+  uint8_t* alpha_trace;   /* [B*trace_len*2] or NULL */
+  int32_t trace_len;
+  int32_t pad_;
+} mcpx_out;
+
+int mcpx_version(void);
+const char* mcpx_last_error(void);
+void mcpx_default_params(mcpx_params* prm);
+/* θ dimension p of a family at (n, m); < 0 on bad input. */
+int64_t mcpx_theta_dim(int32_t family, int32_t n, int32_t m);
+/* number of visible HIP devices (0 when none) */
+int mcpx_device_count(void);
+
+/* Host-buffer batched solve (what the Julia ccall / Python API drive).
+ * Copies θ (and optional warm starts x0/y0/s0, each [B*n] / [B*m], NULL ⇒
+ * the defaults x₀=0, y₀=1, s₀=1 of src/solver.jl:39-41) to `num_devices`
+ * GPUs (0 ⇒ all visible), shards the batch contiguously, solves and copies
+ * the outputs back.  Blocking. */
+int mcpx_solve_batch(const mcpx_desc* desc, const double* theta,
+                     const double* x0, const double* y0, const double* s0,
+                     const mcpx_params* prm, int num_devices, mcpx_out* out);
+
+/* Device-buffer batched solve on the current device: every pointer in the
+ * call (theta, x0/y0/s0 and every mcpx_out array) is device memory.
+ * Enqueued on `stream` (a hipStream_t; NULL = default stream); returns
+ * without synchronising.  This is the hot path the benchmark times. */
+int mcpx_solve_batch_device(const mcpx_desc* desc, const double* theta,
+                            const double* x0, const double* y0, const double* s0,
+                            const mcpx_params* prm, const mcpx_out* out,
+                            void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MCPX_H */

@@ -1,0 +1,84 @@
+"""ctypes mirror of include/mcpx.h (struct layouts and constants only — no loading)."""
+
+import ctypes as C
+
+MCPX_OK = 0
+MCPX_EINVAL = -1
+MCPX_EHIP = -2
+MCPX_ENODEV = -3
+MCPX_EUNSUPPORTED = -4
+
+STATUS_SOLVED = 0
+STATUS_FAILED = 1
+
+FAMILY_QP = 0
+FAMILY_AFFINE = 1
+
+MAX_KKT_DIM = 64
+MAX_INNER_ITERS = 128
+MAX_LS_TRIALS = 64
+
+ERRORS = {
+    MCPX_EINVAL: "invalid argument",
+    MCPX_EHIP: "HIP runtime error",
+    MCPX_ENODEV: "no usable gfx950 device",
+    MCPX_EUNSUPPORTED: "unsupported size",
+}
+
+
+class Params(C.Structure):
+    """mcpx_params — solver keyword arguments (reference src/solver.jl:42-50)."""
+
+    _fields_ = [
+        ("tol", C.c_double),
+        ("tightening_rate", C.c_double),
+        ("loosening_rate", C.c_double),
+        ("min_stepsize", C.c_double),
+        ("tau", C.c_double),
+        ("decay", C.c_double),
+        ("max_inner_iters", C.c_int32),
+        ("max_outer_iters", C.c_int32),
+    ]
+
+
+class Desc(C.Structure):
+    _fields_ = [
+        ("family", C.c_int32),
+        ("n", C.c_int32),
+        ("m", C.c_int32),
+        ("pad_", C.c_int32),
+        ("batch", C.c_int64),
+        ("theta_ld", C.c_int64),
+    ]
+
+
+class Out(C.Structure):
+    _fields_ = [
+        ("x", C.c_void_p),
+        ("y", C.c_void_p),
+        ("s", C.c_void_p),
+        ("kkt_error", C.c_void_p),
+        ("eps", C.c_void_p),
+        ("outer_iters", C.c_void_p),
+        ("status", C.c_void_p),
+        ("newton_iters", C.c_void_p),
+        ("active_mask", C.c_void_p),
+        ("alpha_trace", C.c_void_p),
+        ("trace_len", C.c_int32),
+        ("pad_", C.c_int32),
+    ]
+
+
+def make_params(tol=1e-4, max_inner_iters=20, max_outer_iters=50, tightening_rate=0.1,
+                loosening_rate=0.5, min_stepsize=1e-4, tau=0.995, decay=0.5) -> Params:
+    """Defaults exactly as src/solver.jl:42-48 and :127."""
+    return Params(float(tol), float(tightening_rate), float(loosening_rate), float(min_stepsize),
+                  float(tau), float(decay), int(max_inner_iters), int(max_outer_iters))
+
+
+def theta_dim(family: int, n: int, m: int) -> int:
+    if family == FAMILY_QP:
+        return n * n + m * n + m + n
+    if family == FAMILY_AFFINE:
+        return n * n + 2 * n * m + m * m + n + m
+    raise ValueError(f"unknown family {family}")

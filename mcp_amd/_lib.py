@@ -1,0 +1,59 @@
+"""Loader for the in-tree HIP extension mcp_amd/libmcpx.so (C ABI: include/mcpx.h).
+
+The product path has no CPU fallback: if the library is missing or no gfx950
+device is visible, calls fail loudly (MCPXError).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmcpx.so")
+_lib = None
+
+
+class MCPXError(RuntimeError):
+    """Raised for a negative return code of the C ABI (API misuse / HIP error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mcpx error {code} ({_abi.ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+EXPORTS = ("mcpx_version", "mcpx_last_error", "mcpx_default_params", "mcpx_theta_dim",
+           "mcpx_device_count", "mcpx_solve_batch", "mcpx_solve_batch_device")
+
+
+def lib():
+    """Load libmcpx.so (building it first if only the sources are present)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        from . import build as _build
+        _build.build()
+    L = C.CDLL(LIB_PATH)
+    L.mcpx_version.restype = C.c_int
+    L.mcpx_last_error.restype = C.c_char_p
+    L.mcpx_default_params.argtypes = [C.POINTER(_abi.Params)]
+    L.mcpx_theta_dim.restype = C.c_int64
+    L.mcpx_theta_dim.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    L.mcpx_device_count.restype = C.c_int
+    L.mcpx_solve_batch.restype = C.c_int
+    L.mcpx_solve_batch.argtypes = [C.POINTER(_abi.Desc), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.POINTER(_abi.Params), C.c_int, C.POINTER(_abi.Out)]
+    L.mcpx_solve_batch_device.restype = C.c_int
+    L.mcpx_solve_batch_device.argtypes = [C.POINTER(_abi.Desc), C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.POINTER(_abi.Params), C.POINTER(_abi.Out),
+                                          C.c_void_p]
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise MCPXError(rc, lib().mcpx_last_error().decode(errors="replace"))

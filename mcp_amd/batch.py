@@ -1,0 +1,105 @@
+"""Batched solves through the C ABI (include/mcpx.h).
+
+Two entry points, both running the HIP kernel (never a CPU fallback):
+
+* :func:`solve_batch` — numpy host arrays in, numpy arrays out
+  (``mcpx_solve_batch``: H→D copy, solve, D→H copy; shards over GPUs).
+* :func:`solve_batch_device` — torch device tensors in and out, enqueued on
+  the current HIP stream (``mcpx_solve_batch_device``); the benchmark's hot path.
+
+Both return the per-instance fields of the reference's result NamedTuple
+(src/solver.jl:121: status, x, y, s, kkt_error, ϵ, outer_iters) plus
+``newton_iters``, ``active_mask`` and an optional ``alpha_trace``.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._lib import check, lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def _params(params=None, **kw) -> _abi.Params:
+    return params if params is not None else _abi.make_params(**kw)
+
+
+def solve_batch(family: int, n: int, m: int, theta, *, x0=None, y0=None, s0=None, params=None,
+                num_devices: int = 0, trace_len: int = 0, **kw) -> dict:
+    """Solve B instances on the GPU(s).  theta: (B, ≥p) float64 host array."""
+    theta = np.ascontiguousarray(theta, dtype=np.float64)
+    if theta.ndim == 1:
+        theta = theta[None, :]
+    B, ld = theta.shape
+    prm = _params(params, **kw)
+    conv = lambda a, k: None if a is None else np.ascontiguousarray(np.broadcast_to(a, (B, k)), dtype=np.float64)
+    x0, y0, s0 = conv(x0, n), conv(y0, m), conv(s0, m)
+    words = max(1, (m + 63) // 64)
+    r = dict(
+        x=np.empty((B, n)), y=np.empty((B, m)), s=np.empty((B, m)), kkt_error=np.empty(B),
+        eps=np.empty(B), outer_iters=np.empty(B, np.int32), status=np.empty(B, np.int32),
+        newton_iters=np.empty(B, np.int32),
+        active_mask=np.empty((B, words), np.uint64) if m <= 64 else None,
+        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+    )
+    out = _abi.Out(_ptr(r["x"]), _ptr(r["y"]), _ptr(r["s"]), _ptr(r["kkt_error"]), _ptr(r["eps"]),
+                   _ptr(r["outer_iters"]), _ptr(r["status"]), _ptr(r["newton_iters"]),
+                   _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
+                   int(trace_len), 0)
+    desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
+    check(lib().mcpx_solve_batch(C.byref(desc), _ptr(theta), _ptr(x0), _ptr(y0), _ptr(s0),
+                                 C.byref(prm), int(num_devices), C.byref(out)))
+    return r
+
+
+def alloc_device_outputs(B: int, n: int, m: int, device, trace_len: int = 0, newton: bool = True,
+                         active: bool = True) -> dict:
+    import torch
+
+    f64 = dict(dtype=torch.float64, device=device)
+    i32 = dict(dtype=torch.int32, device=device)
+    return dict(
+        x=torch.empty(B, n, **f64), y=torch.empty(B, m, **f64), s=torch.empty(B, m, **f64),
+        kkt_error=torch.empty(B, **f64), eps=torch.empty(B, **f64),
+        outer_iters=torch.empty(B, **i32), status=torch.empty(B, **i32),
+        newton_iters=torch.empty(B, **i32) if newton else None,
+        active_mask=torch.empty(B, dtype=torch.int64, device=device) if (active and m <= 64) else None,
+        alpha_trace=torch.full((B, trace_len, 2), 254, dtype=torch.uint8, device=device) if trace_len > 0 else None,
+    )
+
+
+def solve_batch_device(family: int, n: int, m: int, theta, out: dict | None = None, *, x0=None, y0=None,
+                       s0=None, params=None, trace_len: int = 0, stream=None, **kw) -> dict:
+    """Enqueue a batched solve on torch device tensors (no synchronisation).
+
+    theta: (B, ≥p) contiguous float64 CUDA(HIP) tensor.  `out` (from
+    :func:`alloc_device_outputs`) is reused when given — nothing is allocated
+    on the hot path then.
+    """
+    import torch
+
+    if not (theta.is_cuda and theta.dtype == torch.float64 and theta.dim() == 2 and theta.is_contiguous()):
+        raise ValueError("theta must be a contiguous (B, p) float64 device tensor")
+    B, ld = theta.shape
+    if out is None:
+        out = alloc_device_outputs(B, n, m, theta.device, trace_len)
+    for t in (x0, y0, s0):
+        if t is not None and not (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()):
+            raise ValueError("warm starts must be contiguous float64 device tensors")
+    dp = lambda t: None if t is None else t.data_ptr()
+    tl = 0 if out.get("alpha_trace") is None else out["alpha_trace"].shape[1]
+    o = _abi.Out(dp(out["x"]), dp(out["y"]), dp(out["s"]), dp(out["kkt_error"]), dp(out["eps"]),
+                 dp(out["outer_iters"]), dp(out["status"]), dp(out.get("newton_iters")),
+                 dp(out.get("active_mask")), dp(out.get("alpha_trace")), int(tl), 0)
+    prm = _params(params, **kw)
+    desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
+    st = stream if stream is not None else torch.cuda.current_stream(theta.device)
+    check(lib().mcpx_solve_batch_device(C.byref(desc), dp(theta), dp(x0), dp(y0), dp(s0), C.byref(prm),
+                                        C.byref(o), C.c_void_p(st.cuda_stream)))
+    return out

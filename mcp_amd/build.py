@@ -1,0 +1,61 @@
+"""In-tree build of the HIP extension libmcpx.so (gfx950 only).
+
+    python -m mcp_amd.build            # build if sources are newer than the .so
+    python -m mcp_amd.build --force
+
+Both translation units are compiled with -ffp-contract=off: the kernels'
+arithmetic contract (explicit fma only) is what makes them bit-identical to
+the oracle.  hipcc cross-compiles for gfx950 without a GPU present.
+"""
+
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libmcpx.so")
+SOURCES = [os.path.join(CSRC, f) for f in ("ipm_kernel.hip", "mcpx_api.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, "ipm_kernel.h"), os.path.join(ROOT, "include", "mcpx.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
+         "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(p) > t for p in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
+    if not force and not _stale():
+        return LIB
+    objs = []
+    t0 = time.time()
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        cmd = [HIPCC, *FLAGS, *extra_flags, "-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    if verbose:
+        print(f"built {LIB} in {time.time() - t0:.1f}s", flush=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True,
+          extra_flags=["-Rpass-analysis=kernel-resource-usage"] if "--resources" in sys.argv else [])

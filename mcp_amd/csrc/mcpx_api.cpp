@@ -1,0 +1,281 @@
+// mcpx_api.cpp — implementation of the C ABI declared in include/mcpx.h.
+//
+// Host side of the drop-in boundary for src/solver.jl:35-122: argument checks
+// (the reference's own ArgumentError / @assert sites, src/AutoDiff.jl:19-23,
+// src/mcp.jl:191), the per-call constant tables the reference computes inline
+// (line-search step sizes src/solver.jl:127-138, ϵ-schedule factors
+// src/solver.jl:111-113), device selection, batch sharding over GPUs and
+// stream-ordered launches.  Reentrant: no global mutable state apart from the
+// thread-local error string.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/mcpx.h"
+#include "ipm_kernel.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(MCPX_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));            \
+  } while (0)
+
+int check_device(int dev) {
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(MCPX_ENODEV, "device %d is %s; this build targets gfx950 (MI355X) only", dev,
+                prop.gcnArchName);
+  return MCPX_OK;
+}
+
+// MCPX_GENERIC_KERNELS=1 disables the compile-time-(n, m) kernels (A/B switch).
+bool specialized_enabled() {
+  const char* e = std::getenv("MCPX_GENERIC_KERNELS");
+  return !(e && e[0] == '1');
+}
+
+int pick_nmax(int N) {
+  if (N <= 8) return 8;
+  if (N <= 16) return 16;
+  if (N <= 32) return 32;
+  if (N <= 64) return 64;
+  return -1;
+}
+
+// Validates desc/params and fills the scalar part + tables of the kernel args.
+int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* nmax) {
+  if (!d || !p) return fail(MCPX_EINVAL, "desc and params must be non-NULL");
+  const int64_t pd = mcpx_theta_dim(d->family, d->n, d->m);
+  if (pd < 0) return fail(MCPX_EINVAL, "bad family %d or negative dimensions (n=%d, m=%d)", d->family, d->n, d->m);
+  if (d->n + d->m < 1) return fail(MCPX_EINVAL, "empty problem (n = m = 0)");
+  if (d->batch < 0) return fail(MCPX_EINVAL, "negative batch");
+  if (d->theta_ld < pd) return fail(MCPX_EINVAL, "theta_ld %lld < parameter dimension %lld", (long long)d->theta_ld, (long long)pd);
+  const int N = d->n + 2 * d->m;
+  *nmax = pick_nmax(N);
+  if (*nmax < 0) return fail(MCPX_EUNSUPPORTED, "KKT dimension %d > %d not supported by the register-resident kernel", N, MCPX_MAX_KKT_DIM);
+  if (!(p->tol > 0) || !(p->min_stepsize > 0) || !(p->decay > 0 && p->decay < 1) || std::isnan(p->tau) ||
+      std::isnan(p->tightening_rate) || std::isnan(p->loosening_rate) || p->max_inner_iters < 1 ||
+      p->max_outer_iters < 1)
+    return fail(MCPX_EINVAL, "invalid solver parameters (tol>0, min_stepsize>0, 0<decay<1, iteration limits >= 1)");
+  if (p->max_inner_iters > MCPX_MAX_INNER_ITERS)
+    return fail(MCPX_EUNSUPPORTED, "max_inner_iters %d > %d", p->max_inner_iters, MCPX_MAX_INNER_ITERS);
+  std::memset(a, 0, sizeof *a);
+  a->n = d->n;
+  a->m = d->m;
+  a->theta_ld = d->theta_ld;
+  a->max_inner = p->max_inner_iters;
+  a->max_outer = p->max_outer_iters;
+  a->tol = p->tol;
+  a->decay = p->decay;
+  a->c_tau = 1.0 - p->tau;  // src/solver.jl:129 (1 - τ)
+  // src/solver.jl:128-135: trials α = 1, decay, decay², … until α < min_stepsize
+  double al = 1.0;
+  int e = 0;
+  for (;;) {
+    if (e >= MCPX_MAX_LS_TRIALS) return fail(MCPX_EUNSUPPORTED, "min_stepsize/decay need more than %d line-search trials", MCPX_MAX_LS_TRIALS);
+    if (al < p->min_stepsize) break;
+    al *= p->decay;
+    ++e;
+  }
+  a->n_trials = e + 1;
+  for (int k = 0; k <= p->max_inner_iters; ++k) {  // src/solver.jl:111-113
+    a->tight[k] = 1.0 - std::exp(-p->tightening_rate * (double)k);
+    a->loose[k] = 1.0 + std::exp(-p->loosening_rate * (double)k);
+  }
+  return MCPX_OK;
+}
+
+int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
+                  const double* s0, const mcpx_out* o, mcpx::KernelArgs a, int nmax, hipStream_t st) {
+  const int64_t CH = (int64_t)1 << 30;
+  const int n = d->n, m = d->m;
+  for (int64_t b0 = 0; b0 < d->batch; b0 += CH) {
+    const int64_t nb = std::min(CH, d->batch - b0);
+    a.theta = theta + b0 * d->theta_ld;
+    a.x0 = x0 ? x0 + b0 * n : nullptr;
+    a.y0 = y0 ? y0 + b0 * m : nullptr;
+    a.s0 = s0 ? s0 + b0 * m : nullptr;
+    a.x = o->x + b0 * n;
+    a.y = o->y + b0 * m;
+    a.s = o->s + b0 * m;
+    a.kkt_error = o->kkt_error + b0;
+    a.eps = o->eps + b0;
+    a.outer_iters = o->outer_iters + b0;
+    a.status = o->status + b0;
+    a.newton_iters = o->newton_iters ? o->newton_iters + b0 : nullptr;
+    a.active_mask = o->active_mask ? o->active_mask + b0 : nullptr;
+    a.alpha_trace = (o->alpha_trace && o->trace_len > 0) ? o->alpha_trace + b0 * (int64_t)o->trace_len * 2 : nullptr;
+    a.trace_len = o->alpha_trace ? o->trace_len : 0;
+    HIP_TRY(mcpx::launch_ipm(nmax, d->family, a, nb, st, specialized_enabled()));
+  }
+  return MCPX_OK;
+}
+
+bool outputs_ok(const mcpx_out* o) {
+  return o && o->x && o->y && o->s && o->kkt_error && o->eps && o->outer_iters && o->status &&
+         o->trace_len >= 0;
+}
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t count) { return count ? hipMalloc(&p, count * sizeof(T)) : hipSuccess; }
+};
+
+// One device's share of mcpx_solve_batch: instances [b0, b0+nb).
+int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
+                const double* s0, const mcpx_params* prm, mcpx_out* o, int64_t b0, int64_t nb) {
+  HIP_TRY(hipSetDevice(dev));
+  int rc = check_device(dev);
+  if (rc) return rc;
+  mcpx::KernelArgs a;
+  int nmax;
+  if ((rc = prepare(d, prm, &a, &nmax))) return rc;
+  const int n = d->n, m = d->m;
+  if (m > 64 && o->active_mask) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
+  DevBuf<double> th, dx0, dy0, ds0, x, y, s, kkt, eps;
+  DevBuf<int32_t> outer, status, newton;
+  DevBuf<uint64_t> am;
+  DevBuf<uint8_t> tr;
+  HIP_TRY(th.alloc((size_t)nb * d->theta_ld));
+  HIP_TRY(hipMemcpy(th.p, theta + b0 * d->theta_ld, sizeof(double) * (size_t)nb * d->theta_ld, hipMemcpyHostToDevice));
+  if (x0) { HIP_TRY(dx0.alloc((size_t)nb * n)); HIP_TRY(hipMemcpy(dx0.p, x0 + b0 * n, sizeof(double) * nb * n, hipMemcpyHostToDevice)); }
+  if (y0) { HIP_TRY(dy0.alloc((size_t)nb * m)); HIP_TRY(hipMemcpy(dy0.p, y0 + b0 * m, sizeof(double) * nb * m, hipMemcpyHostToDevice)); }
+  if (s0) { HIP_TRY(ds0.alloc((size_t)nb * m)); HIP_TRY(hipMemcpy(ds0.p, s0 + b0 * m, sizeof(double) * nb * m, hipMemcpyHostToDevice)); }
+  HIP_TRY(x.alloc((size_t)nb * n)); HIP_TRY(y.alloc((size_t)nb * m)); HIP_TRY(s.alloc((size_t)nb * m));
+  HIP_TRY(kkt.alloc(nb)); HIP_TRY(eps.alloc(nb)); HIP_TRY(outer.alloc(nb)); HIP_TRY(status.alloc(nb));
+  if (o->newton_iters) HIP_TRY(newton.alloc(nb));
+  if (o->active_mask) HIP_TRY(am.alloc(nb));
+  const bool want_tr = o->alpha_trace && o->trace_len > 0;
+  if (want_tr) HIP_TRY(tr.alloc((size_t)nb * o->trace_len * 2));
+  if (want_tr) HIP_TRY(hipMemset(tr.p, 254, (size_t)nb * o->trace_len * 2));
+  mcpx_out od{};
+  od.x = x.p; od.y = y.p; od.s = s.p; od.kkt_error = kkt.p; od.eps = eps.p;
+  od.outer_iters = outer.p; od.status = status.p; od.newton_iters = newton.p;
+  od.active_mask = am.p; od.alpha_trace = tr.p; od.trace_len = want_tr ? o->trace_len : 0;
+  mcpx_desc dd = *d;
+  dd.batch = nb;
+  if ((rc = launch_chunks(&dd, th.p, dx0.p, dy0.p, ds0.p, &od, a, nmax, nullptr))) return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  auto back = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+    return bytes ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
+  };
+  HIP_TRY(back(o->x + b0 * n, x.p, sizeof(double) * nb * n));
+  HIP_TRY(back(o->y + b0 * m, y.p, sizeof(double) * nb * m));
+  HIP_TRY(back(o->s + b0 * m, s.p, sizeof(double) * nb * m));
+  HIP_TRY(back(o->kkt_error + b0, kkt.p, sizeof(double) * nb));
+  HIP_TRY(back(o->eps + b0, eps.p, sizeof(double) * nb));
+  HIP_TRY(back(o->outer_iters + b0, outer.p, sizeof(int32_t) * nb));
+  HIP_TRY(back(o->status + b0, status.p, sizeof(int32_t) * nb));
+  if (o->newton_iters) HIP_TRY(back(o->newton_iters + b0, newton.p, sizeof(int32_t) * nb));
+  if (o->active_mask) HIP_TRY(back(o->active_mask + b0, am.p, sizeof(uint64_t) * nb));
+  if (want_tr) HIP_TRY(back(o->alpha_trace + b0 * o->trace_len * 2, tr.p, (size_t)nb * o->trace_len * 2));
+  return MCPX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mcpx_version(void) { return MCPX_VERSION; }
+
+const char* mcpx_last_error(void) { return g_err.c_str(); }
+
+void mcpx_default_params(mcpx_params* p) {
+  if (!p) return;
+  p->tol = 1e-4;              // src/solver.jl:42
+  p->max_inner_iters = 20;    // :43
+  p->max_outer_iters = 50;    // :44
+  p->tightening_rate = 0.1;   // :45
+  p->loosening_rate = 0.5;    // :46
+  p->min_stepsize = 1e-4;     // :48
+  p->tau = 0.995;             // :127
+  p->decay = 0.5;             // :127
+}
+
+int64_t mcpx_theta_dim(int32_t family, int32_t n, int32_t m) {
+  if (n < 0 || m < 0) return -1;
+  if (family == MCPX_FAMILY_QP) return (int64_t)n * n + (int64_t)m * n + m + n;
+  if (family == MCPX_FAMILY_AFFINE) return (int64_t)n * n + 2 * (int64_t)n * m + (int64_t)m * m + n + m;
+  return -1;
+}
+
+int mcpx_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+int mcpx_solve_batch_device(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
+                            const double* s0, const mcpx_params* prm, const mcpx_out* o, void* stream) {
+  mcpx::KernelArgs a;
+  int nmax;
+  int rc = prepare(d, prm, &a, &nmax);
+  if (rc) return rc;
+  if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
+  if (d->batch == 0) return MCPX_OK;
+  if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
+  if (o->active_mask && d->m > 64) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if ((rc = check_device(dev))) return rc;
+  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream);
+}
+
+int mcpx_solve_batch(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
+                     const double* s0, const mcpx_params* prm, int num_devices, mcpx_out* o) {
+  mcpx::KernelArgs a;
+  int nmax;
+  int rc = prepare(d, prm, &a, &nmax);
+  if (rc) return rc;
+  if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
+  if (d->batch == 0) return MCPX_OK;
+  if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
+  const int avail = mcpx_device_count();
+  if (avail < 1) return fail(MCPX_ENODEV, "no HIP device visible");
+  if (num_devices <= 0 || num_devices > avail) num_devices = avail;
+  if ((int64_t)num_devices > d->batch) num_devices = (int)d->batch;
+  // contiguous shards: device g gets ⌊B/G⌋ (+1 for g < B mod G)
+  std::vector<int64_t> start(num_devices + 1, 0);
+  for (int g = 0; g < num_devices; ++g)
+    start[g + 1] = start[g] + d->batch / num_devices + (g < d->batch % num_devices ? 1 : 0);
+  if (num_devices == 1) return solve_shard(0, d, theta, x0, y0, s0, prm, o, 0, d->batch);
+  std::vector<int> rcs(num_devices, 0);
+  std::vector<std::string> errs(num_devices);
+  std::vector<std::thread> th;
+  for (int g = 0; g < num_devices; ++g)
+    th.emplace_back([&, g] {
+      rcs[g] = solve_shard(g, d, theta, x0, y0, s0, prm, o, start[g], start[g + 1] - start[g]);
+      if (rcs[g]) errs[g] = g_err;
+    });
+  for (auto& t : th) t.join();
+  for (int g = 0; g < num_devices; ++g)
+    if (rcs[g]) return fail(rcs[g], "device %d: %s", g, errs[g].c_str());
+  return MCPX_OK;
+}
+
+}  // extern "C"

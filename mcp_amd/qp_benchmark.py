@@ -1,0 +1,74 @@
+"""Random convex-QP family of the reference benchmark.
+
+Restates benchmark/quadratic_program_benchmark.jl:
+  - generate_random_parameter (:51-74):  P ~ N(0,1)^{n×n} ⊙ Bernoulli(1−sparsity),
+    M = PᵀP, A ~ N(0,1)^{m×n} ⊙ Bernoulli(1−sparsity), b ~ N(0,1)^m, ϕ ~ N(0,1)^n,
+    θ = [vec(M); vec(A); b; ϕ] (column-major vec, :73);
+  - unpack_parameters (:77-90).
+The reference draws from Julia's MersenneTwister(1) (benchmark/path.jl:14),
+which cannot be reproduced without Julia; we use numpy's PCG64 (host) or
+torch's Philox (device) with a documented seed instead.  θ layout and the
+distribution are identical.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+
+def theta_dim(n: int, m: int) -> int:
+    return n * n + m * n + m + n
+
+
+def generate_random_parameter(rng: np.random.Generator, num_primals: int = 100,
+                              num_inequalities: int = 100, sparsity_rate: float = 0.9,
+                              batch: int | None = None) -> np.ndarray:
+    """One θ (batch=None) or a (batch, p) array of θs, column-major blocks."""
+    n, m = num_primals, num_inequalities
+    B = 1 if batch is None else int(batch)
+    keep = 1.0 - sparsity_rate
+    P = rng.standard_normal((B, n, n))
+    if sparsity_rate > 0:
+        P *= rng.random((B, n, n)) < keep
+    M = np.einsum("bki,bkj->bij", P, P)  # PᵀP
+    A = rng.standard_normal((B, m, n))
+    if sparsity_rate > 0:
+        A *= rng.random((B, m, n)) < keep
+    b = rng.standard_normal((B, m))
+    phi = rng.standard_normal((B, n))
+    theta = np.concatenate([
+        M.transpose(0, 2, 1).reshape(B, n * n),  # vec(M), column-major
+        A.transpose(0, 2, 1).reshape(B, m * n),  # vec(A), column-major
+        b, phi], axis=1)
+    return theta[0] if batch is None else theta
+
+
+def unpack_parameters(theta: np.ndarray, num_primals: int, num_inequalities: int):
+    """(:77-90) → dict(M, A, b, ϕ)."""
+    n, m = num_primals, num_inequalities
+    th = np.asarray(theta)
+    M = th[: n * n].reshape(n, n, order="F")
+    A = th[n * n : n * n + m * n].reshape(m, n, order="F")
+    b = th[n * n + m * n : n * n + m * n + m]
+    phi = th[n * n + m * n + m :]
+    return dict(M=M, A=A, b=b, phi=phi)
+
+
+def generate_random_parameter_torch(generator, num_primals: int, num_inequalities: int,
+                                    batch: int, sparsity_rate: float = 0.0, device="cuda"):
+    """Same distribution and layout, generated directly in device memory with torch
+    (used by bench.py so that 65536×12.7 KB of θ never crosses PCIe)."""
+    import torch
+
+    n, m, B = num_primals, num_inequalities, int(batch)
+    kw = dict(generator=generator, device=device, dtype=torch.float64)
+    P = torch.randn(B, n, n, **kw)
+    A = torch.randn(B, m, n, **kw)
+    if sparsity_rate > 0:
+        P *= (torch.rand(B, n, n, **kw) < 1.0 - sparsity_rate)
+        A *= (torch.rand(B, m, n, **kw) < 1.0 - sparsity_rate)
+    M = torch.bmm(P.transpose(1, 2), P)
+    b = torch.randn(B, m, **kw)
+    phi = torch.randn(B, n, **kw)
+    return torch.cat([M.transpose(1, 2).reshape(B, n * n), A.transpose(1, 2).reshape(B, m * n),
+                      b, phi], dim=1).contiguous()

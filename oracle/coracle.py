@@ -1,0 +1,76 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes wrapper around oracle/_build/libipm_oracle.so (the C restatement of
+src/solver.jl, oracle/ipm_oracle.c).  Used by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg; never by mcp_amd/.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from mcp_amd._abi import Desc, Out, Params, make_params, theta_dim
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libipm_oracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with oracle/Makefile (gcc)."""
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        L.oracle_solve_batch.restype = C.c_int
+        L.oracle_solve_batch.argtypes = [C.POINTER(Desc), C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.POINTER(Params), C.POINTER(Out), C.c_int]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def solve_batch(family: int, n: int, m: int, theta: np.ndarray, *, x0=None, y0=None, s0=None,
+                params: Params | None = None, trace_len: int = 0, nthreads: int = 1, **kw) -> dict:
+    """Batched oracle solve.  theta: (B, p) float64.  Returns a dict of numpy arrays."""
+    theta = np.ascontiguousarray(theta, dtype=np.float64)
+    if theta.ndim == 1:
+        theta = theta[None, :]
+    B, ld = theta.shape
+    p = theta_dim(family, n, m)
+    if ld < p:
+        raise ValueError(f"theta has {ld} columns, family needs {p}")
+    prm = params if params is not None else make_params(**kw)
+    conv = lambda a, k: None if a is None else np.ascontiguousarray(np.broadcast_to(a, (B, k)), dtype=np.float64)
+    x0, y0, s0 = conv(x0, n), conv(y0, m), conv(s0, m)
+    words = max(1, (m + 63) // 64)
+    r = dict(
+        x=np.empty((B, n)), y=np.empty((B, m)), s=np.empty((B, m)), kkt_error=np.empty(B),
+        eps=np.empty(B), outer_iters=np.empty(B, np.int32), status=np.empty(B, np.int32),
+        newton_iters=np.empty(B, np.int32), active_mask=np.empty((B, words), np.uint64),
+        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+    )
+    out = Out(_ptr(r["x"]), _ptr(r["y"]), _ptr(r["s"]), _ptr(r["kkt_error"]), _ptr(r["eps"]),
+              _ptr(r["outer_iters"]), _ptr(r["status"]), _ptr(r["newton_iters"]),
+              _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
+              int(trace_len), 0)
+    desc = Desc(family, n, m, 0, B, ld)
+    rc = lib().oracle_solve_batch(C.byref(desc), _ptr(theta), _ptr(x0), _ptr(y0), _ptr(s0),
+                                  C.byref(prm), C.byref(out), int(nthreads))
+    if rc != 0:
+        raise ValueError(f"oracle_solve_batch failed with code {rc}")
+    return r

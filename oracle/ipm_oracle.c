@@ -1,0 +1,381 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C, single-instance-at-a-time restatement of the reference
+ * interior-point solver of MixedComplementarityProblems.jl (TianyuQ/MCP),
+ * src/solver.jl:35-138, for the problem families of include/mcpx.h.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this; the product path (mcp_amd/) never does.
+ *
+ * Parity status: the reference is Julia and cannot run here (no Julia
+ * toolchain, dependencies not vendored), and it holds no golden vectors.
+ * This restatement is pinned only by the reference's own analytic test
+ * assertions (test/runtests.jl:30-38, :112-114, see tests/test_oracle.py) and
+ * cross-checked against an independent numpy/LAPACK restatement
+ * (oracle/ipm_ref.py).  Iterate-level (1e-8) parity with the Julia solver is
+ * therefore "parity unpinned"; see DESIGN.md §Oracle.
+ *
+ * Arithmetic contract (shared bit-for-bit with the HIP kernel):
+ *  - residual F per src/mcp.jl:76-80 with z = [x; y; s] (src/mcp.jl:74);
+ *    dot products are fma chains in ascending column order;
+ *  - Jacobian per src/mcp.jl:97-120 plus tol·I on the whole diagonal
+ *    (src/solver.jl:81);
+ *  - the Newton system is solved by dense LU with partial pivoting on the
+ *    augmented matrix [∇F + tol·I | −F]: rows are never physically swapped;
+ *    the pivot of column k is the first remaining row (ascending index) of
+ *    largest |a_ik| (NaN never wins; if all remaining are NaN the first
+ *    remaining row is taken); an exactly-zero pivot is the linear-solve
+ *    failure (the UMFPACK "singular" retcode of src/solver.jl:84);
+ *    elimination a_ij ← fma(−l_i, u_j, a_ij) with l_i = a_ik / pivot;
+ *    back substitution column-oriented with x_k = b_p / u_pk;
+ *    (UMFPACK itself, LinearSolve 2.38 UMFPACKFactorization, is a third-party
+ *    sparse LU not present here: this dense LU replaces it, results differ in
+ *    rounding only);
+ *  - line search α = decayᵉ by repeated multiplication, predicate
+ *    v + α·δ < (1−τ)·v evaluated without contraction (src/solver.jl:127-138);
+ *  - ϵ factors 1 − exp(−t·k) / 1 + exp(−l·k) from libm (src/solver.jl:111-113).
+ * Build with -ffp-contract=off (oracle/Makefile) so that only the explicit
+ * fma() calls fuse.
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/mcpx.h"
+
+typedef struct oracle_tables {
+  double alpha[MCPX_MAX_LS_TRIALS];
+  int n_trials; /* E + 1 */
+  double c_tau; /* (1 - τ) */
+  double tight[MCPX_MAX_INNER_ITERS + 1];
+  double loose[MCPX_MAX_INNER_ITERS + 1];
+} oracle_tables;
+
+/* Validates the keyword arguments and precomputes what the reference computes
+ * inline.  Returns 0 or MCPX_EINVAL / MCPX_EUNSUPPORTED. */
+int oracle_build_tables(const mcpx_params* p, oracle_tables* t) {
+  if (!(p->tol > 0) || !(p->min_stepsize > 0) || !(p->decay > 0 && p->decay < 1) ||
+      !(p->tau == p->tau) || !(p->tightening_rate == p->tightening_rate) ||
+      !(p->loosening_rate == p->loosening_rate) || p->max_inner_iters < 1 ||
+      p->max_outer_iters < 1)
+    return MCPX_EINVAL;
+  if (p->max_inner_iters > MCPX_MAX_INNER_ITERS) return MCPX_EUNSUPPORTED;
+  /* src/solver.jl:128-135: α = 1; while violated: if α < tol → NaN; α *= decay */
+  double a = 1.0;
+  int e = 0;
+  for (;;) {
+    if (e >= MCPX_MAX_LS_TRIALS) return MCPX_EUNSUPPORTED;
+    t->alpha[e] = a;
+    if (a < p->min_stepsize) break;
+    a *= p->decay;
+    ++e;
+  }
+  t->n_trials = e + 1;
+  t->c_tau = 1.0 - p->tau; /* src/solver.jl:129 (1 - τ) */
+  for (int k = 0; k <= p->max_inner_iters; ++k) {
+    /* src/solver.jl:111-113 */
+    t->tight[k] = 1.0 - exp(-p->tightening_rate * (double)k);
+    t->loose[k] = 1.0 + exp(-p->loosening_rate * (double)k);
+  }
+  return 0;
+}
+
+/* ---- problem families: residual row + Jacobian row (src/mcp.jl:72-120) ---- */
+
+/* Row i of F and of ∇F (without tol·I) at z = [x; y; s]. */
+static double family_row(int family, int n, int m, const double* th, const double* z,
+                         double eps, int i, double* row) {
+  const int N = n + 2 * m;
+  const double* x = z;
+  const double* y = z + n;
+  const double* s = z + n + m;
+  for (int j = 0; j < N; ++j) row[j] = 0.0;
+  if (i < n) { /* G rows */
+    double acc = 0.0;
+    if (family == MCPX_FAMILY_QP) {
+      /* G = M x − ϕ − Aᵀ y (benchmark/quadratic_program_benchmark.jl:12-32) */
+      const double* M = th;
+      const double* A = th + (size_t)n * n;
+      const double* phi = th + (size_t)n * n + (size_t)m * n + m;
+      for (int j = 0; j < n; ++j) {
+        row[j] = M[(size_t)j * n + i];
+        acc = fma(row[j], x[j], acc);
+      }
+      for (int k = 0; k < m; ++k) {
+        row[n + k] = -A[(size_t)i * m + k];
+        acc = fma(row[n + k], y[k], acc);
+      }
+      return acc - phi[i];
+    } else { /* G = P x + Q y + g */
+      const double* P = th;
+      const double* Q = th + (size_t)n * n;
+      const double* g = th + (size_t)n * n + 2 * (size_t)n * m + (size_t)m * m;
+      for (int j = 0; j < n; ++j) {
+        row[j] = P[(size_t)j * n + i];
+        acc = fma(row[j], x[j], acc);
+      }
+      for (int k = 0; k < m; ++k) {
+        row[n + k] = Q[(size_t)k * n + i];
+        acc = fma(row[n + k], y[k], acc);
+      }
+      return acc + g[i];
+    }
+  } else if (i < n + m) { /* H − s rows */
+    const int k = i - n;
+    double acc = 0.0;
+    row[n + m + k] = -1.0;
+    if (family == MCPX_FAMILY_QP) {
+      const double* A = th + (size_t)n * n;
+      const double* b = th + (size_t)n * n + (size_t)m * n;
+      for (int j = 0; j < n; ++j) {
+        row[j] = A[(size_t)j * m + k];
+        acc = fma(row[j], x[j], acc);
+      }
+      return (acc - b[k]) - s[k];
+    } else {
+      const double* R = th + (size_t)n * n + (size_t)n * m;
+      const double* S = th + (size_t)n * n + 2 * (size_t)n * m;
+      const double* h = th + (size_t)n * n + 2 * (size_t)n * m + (size_t)m * m + n;
+      for (int j = 0; j < n; ++j) {
+        row[j] = R[(size_t)j * m + k];
+        acc = fma(row[j], x[j], acc);
+      }
+      for (int q = 0; q < m; ++q) {
+        row[n + q] = S[(size_t)q * m + k];
+        acc = fma(row[n + q], y[q], acc);
+      }
+      return (acc + h[k]) - s[k];
+    }
+  } else { /* s ⊙ y − ϵ rows */
+    const int k = i - n - m;
+    row[n + k] = s[k];
+    row[n + m + k] = y[k];
+    return s[k] * y[k] - eps;
+  }
+}
+
+/* ---- dense LU with partial pivoting on [J | b]; returns 0 ok, 1 singular ---- */
+static int lu_solve(int N, double* J /* N×N row-major, destroyed */, double* b /* destroyed */,
+                    double* dz, int* remaining, int* step_of, int* prow) {
+  for (int i = 0; i < N; ++i) remaining[i] = 1;
+  for (int k = 0; k < N; ++k) {
+    int best = -1;
+    double bv = -1.0;
+    for (int i = 0; i < N; ++i) {
+      if (!remaining[i]) continue;
+      const double v = fabs(J[(size_t)i * N + k]);
+      if (v > bv) { bv = v; best = i; }
+    }
+    if (best < 0)
+      for (int i = 0; i < N; ++i)
+        if (remaining[i]) { best = i; break; }
+    const double piv = J[(size_t)best * N + k];
+    if (piv == 0.0) return 1;
+    remaining[best] = 0;
+    step_of[best] = k;
+    prow[k] = best;
+    const double* u = J + (size_t)best * N;
+    for (int i = 0; i < N; ++i) {
+      if (!remaining[i]) continue;
+      double* a = J + (size_t)i * N;
+      const double l = a[k] / piv;
+      for (int j = k + 1; j < N; ++j) a[j] = fma(-l, u[j], a[j]);
+      b[i] = fma(-l, b[best], b[i]);
+    }
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    const int p = prow[k];
+    const double xk = b[p] / J[(size_t)p * N + k];
+    dz[k] = xk;
+    for (int i = 0; i < N; ++i)
+      if (step_of[i] < k) b[i] = fma(-J[(size_t)i * N + k], xk, b[i]);
+  }
+  return 0;
+}
+
+/* first e in [0, n_trials) with no violation, or -1 (the NaN of src/solver.jl:131) */
+static int linesearch_exponent(const double* v, const double* d, int cnt, const oracle_tables* t) {
+  for (int e = 0; e < t->n_trials; ++e) {
+    const double a = t->alpha[e];
+    int viol = 0;
+    for (int i = 0; i < cnt; ++i) {
+      const double lhs = v[i] + a * d[i];
+      const double rhs = t->c_tau * v[i];
+      if (lhs < rhs) { viol = 1; break; }
+    }
+    if (!viol) return e;
+  }
+  return -1;
+}
+
+typedef struct ws {
+  double *J, *row, *F, *b, *dz, *z;
+  int *remaining, *step_of, *prow;
+} ws;
+
+static int ws_alloc(ws* w, int N) {
+  w->J = (double*)malloc(sizeof(double) * (size_t)N * N);
+  w->row = (double*)malloc(sizeof(double) * N);
+  w->F = (double*)malloc(sizeof(double) * N);
+  w->b = (double*)malloc(sizeof(double) * N);
+  w->dz = (double*)malloc(sizeof(double) * N);
+  w->z = (double*)malloc(sizeof(double) * N);
+  w->remaining = (int*)malloc(sizeof(int) * N);
+  w->step_of = (int*)malloc(sizeof(int) * N);
+  w->prow = (int*)malloc(sizeof(int) * N);
+  return (w->J && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
+}
+static void ws_free(ws* w) {
+  free(w->J); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
+  free(w->remaining); free(w->step_of); free(w->prow);
+}
+
+/* One instance: src/solver.jl:35-122. */
+static void solve_one(const mcpx_desc* d, const double* th, const double* x0, const double* y0,
+                      const double* s0, const mcpx_params* p, const oracle_tables* t, ws* w,
+                      int64_t inst, const mcpx_out* o) {
+  const int n = d->n, m = d->m, N = n + 2 * m;
+  double* z = w->z;
+  /* src/solver.jl:39-41,64-66 */
+  for (int i = 0; i < n; ++i) z[i] = x0 ? x0[inst * n + i] : 0.0;
+  for (int k = 0; k < m; ++k) z[n + k] = y0 ? y0[inst * m + k] : 1.0;
+  for (int k = 0; k < m; ++k) z[n + m + k] = s0 ? s0[inst * m + k] : 1.0;
+  double eps = 1.0;           /* :67 */
+  double kkt = INFINITY;      /* :68 */
+  int status = MCPX_STATUS_SOLVED; /* :69 */
+  int outer = 1;              /* :70 */
+  int newton = 0;
+  while (kkt > p->tol && eps > p->tol && outer < p->max_outer_iters) { /* :71 */
+    int inner = 1;            /* :72 */
+    status = MCPX_STATUS_SOLVED; /* :73 */
+    while (kkt > eps && inner < p->max_inner_iters) { /* :75 */
+      /* :79-82 F!, ∇F_z!, A = ∇F + tol I, b = −F */
+      for (int i = 0; i < N; ++i) {
+        w->F[i] = family_row(d->family, n, m, th, z, eps, i, w->J + (size_t)i * N);
+        w->J[(size_t)i * N + i] += p->tol;
+        w->b[i] = -w->F[i];
+      }
+      /* :83-88 */
+      if (lu_solve(N, w->J, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
+        status = MCPX_STATUS_FAILED;
+        break;
+      }
+      /* :93-100 */
+      const int es = linesearch_exponent(z + n + m, w->dz + n + m, m, t);
+      const int ey = linesearch_exponent(z + n, w->dz + n, m, t);
+      if (es < 0 || ey < 0) {
+        status = MCPX_STATUS_FAILED;
+        break;
+      }
+      if (o->alpha_trace && newton < o->trace_len) { /* accepted steps only */
+        uint8_t* tr = o->alpha_trace + ((size_t)inst * o->trace_len + newton) * 2;
+        tr[0] = (uint8_t)es;
+        tr[1] = (uint8_t)ey;
+      }
+      const double as = t->alpha[es], ay = t->alpha[ey];
+      /* :103-105 (x moves with α_s) */
+      for (int i = 0; i < n; ++i) z[i] = z[i] + as * w->dz[i];
+      for (int k = 0; k < m; ++k) z[n + m + k] = z[n + m + k] + as * w->dz[n + m + k];
+      for (int k = 0; k < m; ++k) z[n + k] = z[n + k] + ay * w->dz[n + k];
+      /* :107 kkt_error = ‖F‖∞ of the pre-step F, NaN-propagating */
+      double mx = fabs(w->F[0]);
+      for (int i = 1; i < N; ++i) {
+        const double v = fabs(w->F[i]);
+        if (v != v || v > mx) mx = v;
+        if (mx != mx) break;
+      }
+      kkt = mx;
+      ++inner;
+      ++newton;
+    }
+    eps *= (status == MCPX_STATUS_SOLVED) ? t->tight[inner] : t->loose[inner]; /* :111-113 */
+    ++outer; /* :114 */
+  }
+  if (outer == p->max_outer_iters) status = MCPX_STATUS_FAILED; /* :117-119 */
+  for (int i = 0; i < n; ++i) o->x[inst * n + i] = z[i];
+  for (int k = 0; k < m; ++k) o->y[inst * m + k] = z[n + k];
+  for (int k = 0; k < m; ++k) o->s[inst * m + k] = z[n + m + k];
+  o->kkt_error[inst] = kkt;
+  o->eps[inst] = eps;
+  o->outer_iters[inst] = outer;
+  o->status[inst] = status;
+  if (o->newton_iters) o->newton_iters[inst] = newton;
+  if (o->active_mask) {
+    const int words = m > 64 ? (m + 63) / 64 : 1;
+    uint64_t* am = o->active_mask + (size_t)inst * words;
+    for (int q = 0; q < words; ++q) am[q] = 0;
+    for (int k = 0; k < m; ++k)
+      if (z[n + k] > z[n + m + k]) am[k / 64] |= (uint64_t)1 << (k % 64);
+  }
+}
+
+typedef struct job {
+  const mcpx_desc* d;
+  const double *theta, *x0, *y0, *s0;
+  const mcpx_params* p;
+  const oracle_tables* t;
+  const mcpx_out* o;
+  int64_t next; /* shared work counter */
+  pthread_mutex_t mu;
+  int err;
+} job;
+
+static void* worker(void* arg) {
+  job* j = (job*)arg;
+  ws w;
+  if (ws_alloc(&w, j->d->n + 2 * j->d->m)) {
+    pthread_mutex_lock(&j->mu);
+    j->err = 1;
+    pthread_mutex_unlock(&j->mu);
+    ws_free(&w);
+    return NULL;
+  }
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    const int64_t b = j->next++;
+    pthread_mutex_unlock(&j->mu);
+    if (b >= j->d->batch) break;
+    solve_one(j->d, j->theta + b * j->d->theta_ld, j->x0, j->y0, j->s0, j->p, j->t, &w, b, j->o);
+  }
+  ws_free(&w);
+  return NULL;
+}
+
+int64_t oracle_theta_dim(int family, int n, int m) {
+  if (n < 0 || m < 0) return -1;
+  if (family == MCPX_FAMILY_QP) return (int64_t)n * n + (int64_t)m * n + m + n;
+  if (family == MCPX_FAMILY_AFFINE) return (int64_t)n * n + 2 * (int64_t)n * m + (int64_t)m * m + n + m;
+  return -1;
+}
+
+/* Batched entry: same argument meaning as mcpx_solve_batch (host buffers),
+ * instances distributed over `nthreads` POSIX threads (one instance per task). */
+int oracle_solve_batch(const mcpx_desc* d, const double* theta, const double* x0,
+                       const double* y0, const double* s0, const mcpx_params* p,
+                       mcpx_out* o, int nthreads) {
+  if (!d || !theta || !p || !o || !o->x || !o->y || !o->s || !o->kkt_error || !o->eps ||
+      !o->outer_iters || !o->status)
+    return MCPX_EINVAL;
+  const int64_t pd = oracle_theta_dim(d->family, d->n, d->m);
+  if (pd < 0 || d->n + d->m < 1 || d->batch < 0 || d->theta_ld < pd) return MCPX_EINVAL;
+  oracle_tables t;
+  const int rc = oracle_build_tables(p, &t);
+  if (rc) return rc;
+  job j;
+  j.d = d; j.theta = theta; j.x0 = x0; j.y0 = y0; j.s0 = s0; j.p = p; j.t = &t; j.o = o;
+  j.next = 0; j.err = 0;
+  pthread_mutex_init(&j.mu, NULL);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads == 1) {
+    worker(&j);
+  } else {
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+    for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, worker, &j);
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    free(th);
+  }
+  pthread_mutex_destroy(&j.mu);
+  return j.err ? MCPX_EINVAL : 0;
+}

@@ -1,0 +1,147 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+Independent numpy/LAPACK restatement of the reference interior-point solver
+(MixedComplementarityProblems.jl, src/solver.jl:35-138), written directly from
+the Julia source and sharing no code with oracle/ipm_oracle.c.  It differs from
+the C oracle deliberately in the one place the reference itself is
+implementation-defined — the Newton linear solve: the reference calls UMFPACK
+through LinearSolve.jl (src/solver.jl:50,61,83), this module calls LAPACK
+dgetrf/dgetrs (scipy.linalg.lu_factor) on the dense ∇F + tol·I, the C oracle
+uses its own unblocked LU.  Agreement of the two is therefore evidence that the
+C oracle restates the reference *algorithm* (loop bounds, ϵ schedule, line
+search, update order, status logic), independent of LU rounding.
+
+Used only by tests/ (never by the product package mcp_amd/).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import scipy.linalg
+
+QP, AFFINE = 0, 1
+
+
+def theta_dim(family: int, n: int, m: int) -> int:
+    if family == QP:  # benchmark/quadratic_program_benchmark.jl:77-90
+        return n * n + m * n + m + n
+    return n * n + 2 * n * m + m * m + n + m
+
+
+def unpack(family: int, theta: np.ndarray, n: int, m: int):
+    """θ → (P, Q, R, S, g, h) with G = P x + Q y + g, H = R x + S y + h."""
+    th = np.asarray(theta, dtype=np.float64)
+    if family == QP:
+        # unpack_parameters, benchmark/quadratic_program_benchmark.jl:77-90 (column-major)
+        M = th[: n * n].reshape(n, n, order="F")
+        A = th[n * n : n * n + m * n].reshape(m, n, order="F")
+        b = th[n * n + m * n : n * n + m * n + m]
+        phi = th[n * n + m * n + m : n * n + m * n + m + n]
+        # G = M x − ϕ − Aᵀ y, H = A x − b  (:12-32)
+        return M, -A.T, A, np.zeros((m, m)), -phi, -b
+    o = 0
+    P = th[o : o + n * n].reshape(n, n, order="F"); o += n * n
+    Q = th[o : o + n * m].reshape(n, m, order="F"); o += n * m
+    R = th[o : o + m * n].reshape(m, n, order="F"); o += m * n
+    S = th[o : o + m * m].reshape(m, m, order="F"); o += m * m
+    g = th[o : o + n]; o += n
+    h = th[o : o + m]
+    return P, Q, R, S, g, h
+
+
+def F_and_jacobian(blocks, x, y, s, eps):
+    """F = [G; H − s; s⊙y − ϵ] (src/mcp.jl:76-80) and ∇_z F (src/mcp.jl:97-120)."""
+    P, Q, R, S, g, h = blocks
+    n, m = len(x), len(y)
+    G = P @ x + Q @ y + g
+    H = R @ x + S @ y + h
+    F = np.concatenate([G, H - s, s * y - eps])
+    N = n + 2 * m
+    J = np.zeros((N, N))
+    J[:n, :n] = P
+    J[:n, n : n + m] = Q
+    J[n : n + m, :n] = R
+    J[n : n + m, n : n + m] = S
+    J[n : n + m, n + m :] = -np.eye(m)
+    J[n + m :, n : n + m] = np.diag(s)
+    J[n + m :, n + m :] = np.diag(y)
+    return F, J
+
+
+def fraction_to_the_boundary_linesearch(v, d, tau=0.995, decay=0.5, tol=1e-4):
+    """src/solver.jl:127-138, literally.  Returns (α, number of halvings)."""
+    alpha = 1.0
+    e = 0
+    while np.any(v + alpha * d < (1 - tau) * v):
+        if alpha < tol:
+            return math.nan, -1
+        alpha *= decay
+        e += 1
+    return alpha, e
+
+
+@dataclass
+class Solution:
+    status: str
+    x: np.ndarray
+    y: np.ndarray
+    s: np.ndarray
+    kkt_error: float
+    eps: float
+    outer_iters: int
+    newton_iters: int
+    alpha_trace: list
+
+
+def solve(family, theta, n, m, *, x0=None, y0=None, s0=None, tol=1e-4, max_inner_iters=20,
+          max_outer_iters=50, tightening_rate=0.1, loosening_rate=0.5, min_stepsize=1e-4):
+    """src/solver.jl:35-122 for one instance."""
+    blocks = unpack(family, theta, n, m)
+    N = n + 2 * m
+    x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64)
+    y = np.ones(m) if y0 is None else np.array(y0, dtype=np.float64)
+    s = np.ones(m) if s0 is None else np.array(s0, dtype=np.float64)
+    eps = 1.0
+    kkt_error = math.inf
+    status = "solved"
+    outer_iters = 1
+    newton = 0
+    trace = []
+    while kkt_error > tol and eps > tol and outer_iters < max_outer_iters:
+        inner_iters = 1
+        status = "solved"
+        while kkt_error > eps and inner_iters < max_inner_iters:
+            F, J = F_and_jacobian(blocks, x, y, s, eps)
+            A = J + tol * np.eye(N)
+            try:
+                with np.errstate(all="ignore"):
+                    lu = scipy.linalg.lu_factor(A, check_finite=False)
+                if np.any(np.diag(lu[0]) == 0.0):
+                    raise np.linalg.LinAlgError("singular")
+                dz = scipy.linalg.lu_solve(lu, -F, check_finite=False)
+            except (np.linalg.LinAlgError, ValueError):
+                status = "failed"
+                break
+            dx, dy, ds = dz[:n], dz[n : n + m], dz[n + m :]
+            a_s, es = fraction_to_the_boundary_linesearch(s, ds, tol=min_stepsize)
+            a_y, ey = fraction_to_the_boundary_linesearch(y, dy, tol=min_stepsize)
+            trace.append((es if es >= 0 else 255, ey if ey >= 0 else 255))
+            if math.isnan(a_s) or math.isnan(a_y):
+                status = "failed"
+                break
+            x = x + a_s * dx
+            s = s + a_s * ds
+            y = y + a_y * dy
+            absF = np.abs(F)
+            kkt_error = math.nan if np.any(np.isnan(absF)) else float(absF.max())
+            inner_iters += 1
+            newton += 1
+        eps *= (1 - math.exp(-tightening_rate * inner_iters)) if status == "solved" else (
+            1 + math.exp(-loosening_rate * inner_iters))
+        outer_iters += 1
+    if outer_iters == max_outer_iters:
+        status = "failed"
+    return Solution(status, x, y, s, kkt_error, eps, outer_iters, newton, trace)
