@@ -64,12 +64,24 @@ extern "C" {
 #define MCPX_FAMILY_QP 0
 #define MCPX_FAMILY_AFFINE 1
 
-/* KKT dimension N = n + 2m handled by the register-resident kernels */
+/* largest linear-system dimension of the register-resident kernels
+ * (n + m for MCPX_LINSOLVE_REDUCED, n + 2m for MCPX_LINSOLVE_DENSE) */
 #define MCPX_MAX_KKT_DIM 64
 /* largest max_inner_iters (ϵ-schedule table length) */
 #define MCPX_MAX_INNER_ITERS 128
 /* largest number of line-search trials (α = decayᵉ, e = 0..E) */
 #define MCPX_MAX_LS_TRIALS 64
+
+/* Newton linear solve (∇F + tol·I) δz = −F, src/solver.jl:81-83:
+ *  MCPX_LINSOLVE_REDUCED  exact block elimination of the slack block first —
+ *                         ∂(s⊙y − ϵ)/∂s = Y + tol·I is diagonal for every MCP of
+ *                         the form F = [G; H − s; s⊙y − ϵ] (src/mcp.jl:76-80) —
+ *                         then dense LU with partial pivoting of the (n+m)-dim
+ *                         Schur complement (default; N ≤ 64 means n + m ≤ 64);
+ *  MCPX_LINSOLVE_DENSE    dense LU with partial pivoting of the full
+ *                         (n+2m)-dim system (n + 2m ≤ 64). */
+#define MCPX_LINSOLVE_REDUCED 0
+#define MCPX_LINSOLVE_DENSE 1
 
 /* Solver keyword arguments, same names and defaults as src/solver.jl:42-50;
  * tau and decay are the hard-coded defaults of
@@ -83,6 +95,8 @@ typedef struct mcpx_params {
   double decay;             /* 0.5  */
   int32_t max_inner_iters;  /* 20 */
   int32_t max_outer_iters;  /* 50 */
+  int32_t linear_solver;    /* MCPX_LINSOLVE_* — the reference's linear_solve_algorithm kwarg (src/solver.jl:50) */
+  int32_t pad_;
 } mcpx_params;
 
 /* Batch descriptor. */

@@ -15,6 +15,10 @@ FAMILY_QP = 0
 FAMILY_AFFINE = 1
 
 MAX_KKT_DIM = 64
+
+LINSOLVE_REDUCED = 0
+LINSOLVE_DENSE = 1
+LINEAR_SOLVERS = {"reduced": LINSOLVE_REDUCED, "dense": LINSOLVE_DENSE}
 MAX_INNER_ITERS = 128
 MAX_LS_TRIALS = 64
 
@@ -38,6 +42,8 @@ class Params(C.Structure):
         ("decay", C.c_double),
         ("max_inner_iters", C.c_int32),
         ("max_outer_iters", C.c_int32),
+        ("linear_solver", C.c_int32),
+        ("pad_", C.c_int32),
     ]
 
 
@@ -70,10 +76,13 @@ class Out(C.Structure):
 
 
 def make_params(tol=1e-4, max_inner_iters=20, max_outer_iters=50, tightening_rate=0.1,
-                loosening_rate=0.5, min_stepsize=1e-4, tau=0.995, decay=0.5) -> Params:
-    """Defaults exactly as src/solver.jl:42-48 and :127."""
+                loosening_rate=0.5, min_stepsize=1e-4, tau=0.995, decay=0.5,
+                linear_solver="reduced") -> Params:
+    """Defaults exactly as src/solver.jl:42-48 and :127.  `linear_solver` plays the
+    role of the reference's `linear_solve_algorithm` kwarg (src/solver.jl:50)."""
+    ls = LINEAR_SOLVERS[linear_solver] if isinstance(linear_solver, str) else int(linear_solver)
     return Params(float(tol), float(tightening_rate), float(loosening_rate), float(min_stepsize),
-                  float(tau), float(decay), int(max_inner_iters), int(max_outer_iters))
+                  float(tau), float(decay), int(max_inner_iters), int(max_outer_iters), ls, 0)
 
 
 def theta_dim(family: int, n: int, m: int) -> int:

@@ -24,6 +24,24 @@
 
 #include "ipm_kernel.h"
 
+// Diagnostic phase stamps (tools/phase_profile.hip builds with MCPX_STAMPS=1;
+// the product build compiles them away).
+#ifndef MCPX_STAMPS
+#define MCPX_STAMPS 0
+#endif
+#if MCPX_STAMPS
+#define MCPX_STAMP(i)                                   \
+  do {                                                  \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    st_acc[i] += t_ - st_last;                          \
+    st_last = t_;                                       \
+  } while (0)
+#else
+#define MCPX_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
 namespace mcpx {
 
 namespace {
@@ -32,6 +50,39 @@ __device__ __forceinline__ double bcast(double v, int src) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
   return __hiloint2double(hi, lo);
+}
+
+// Broadcast 4 doubles of lane `p` to the wave through SGPRs.  A dynamic-lane
+// v_readlane costs ≈8.5 cycles per dword on gfx950 (tools/ubench_mfma64.hip);
+// v_readfirstlane under an EXEC mask holding only lane p costs ≈3.5, so the
+// pivot-row broadcast runs with EXEC switched to the pivot lane.  The trailing
+// s_nop 1 covers the VALU-writes-SGPR → VALU-reads-SGPR hazard that hipcc does
+// not see through inline asm.
+__device__ __forceinline__ void bcast4(double v0, double v1, double v2, double v3, uint64_t pmask,
+                                       double& u0, double& u1, double& u2, double& u3) {
+  int o0, o1, o2, o3, o4, o5, o6, o7;
+  uint64_t saved;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[pm]\n\t"
+      "v_readfirstlane_b32 %0, %[a0]\n\t"
+      "v_readfirstlane_b32 %1, %[a1]\n\t"
+      "v_readfirstlane_b32 %2, %[a2]\n\t"
+      "v_readfirstlane_b32 %3, %[a3]\n\t"
+      "v_readfirstlane_b32 %4, %[a4]\n\t"
+      "v_readfirstlane_b32 %5, %[a5]\n\t"
+      "v_readfirstlane_b32 %6, %[a6]\n\t"
+      "v_readfirstlane_b32 %7, %[a7]\n\t"
+      "s_mov_b64 exec, %[sv]\n\t"
+      "s_nop 1"
+      : "=s"(o0), "=s"(o1), "=s"(o2), "=s"(o3), "=s"(o4), "=s"(o5), "=s"(o6), "=s"(o7), [sv] "=&s"(saved)
+      : [a0] "v"(__double2loint(v0)), [a1] "v"(__double2hiint(v0)), [a2] "v"(__double2loint(v1)),
+        [a3] "v"(__double2hiint(v1)), [a4] "v"(__double2loint(v2)), [a5] "v"(__double2hiint(v2)),
+        [a6] "v"(__double2loint(v3)), [a7] "v"(__double2hiint(v3)), [pm] "s"(pmask));
+  u0 = __hiloint2double(o1, o0);
+  u1 = __hiloint2double(o3, o2);
+  u2 = __hiloint2double(o5, o4);
+  u3 = __hiloint2double(o7, o6);
 }
 
 // Wave-wide max of an unsigned 32-bit key, result uniform.  DPP row_shr
@@ -177,6 +228,10 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
   int status = 0;                      // :69
   int outer = 1;                       // :70
   int newton = 0;
+#if MCPX_STAMPS
+  uint64_t st_acc[4] = {0, 0, 0, 0};
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
 
   while (kkt > tol && eps > tol && outer < args.max_outer) {  // :71
     int inner = 1;   // :72
@@ -197,12 +252,13 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       const bool any_nan = ballot(aF != aF) != 0ull;
       const double kkt_step = any_nan ? __builtin_nan("") : wave_max_nonneg(aF);
 
+      MCPX_STAMP(0);
       // ---- dense LU with partial pivoting on [∇F + tol I | −F] (:81-83) --
       uint64_t rem = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
       int my_step = 1 << 30;  // LU step at which this row became a pivot row
       int pk = 0;             // ln k: pivot row of step k
       bool singular = false;
-#pragma unroll
+#pragma clang loop unroll(full)
       for (int k = 0; k < NMAX; ++k) {
         if (k >= N || singular) continue;  // uniform; no `break` so the loop fully unrolls
         const double ak = a[k];
@@ -233,11 +289,28 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
         if (ln == k) pk = p;
         if ((rem >> ln) & 1ull) {
           const double l = ak / piv;
-#pragma unroll
-          for (int j = k + 1; j < NMAX; ++j) a[j] = fma(-l, bcast(a[j], p), a[j]);
-          rhs = fma(-l, bcast(rhs, p), rhs);
+          const uint64_t pm = 1ull << p;
+          // columns k+1 .. NMAX-1 and the right-hand side (index NMAX), 4 per broadcast
+#pragma clang loop unroll(full)
+          for (int g = 0; g <= NMAX / 4; ++g) {
+            if (4 * g + 3 <= k) continue;  // static: group entirely left of the pivot column
+            double v[4], u[4];
+#pragma clang loop unroll(full)
+            for (int t = 0; t < 4; ++t) {
+              const int j = 4 * g + t;
+              v[t] = (j < NMAX) ? a[j < NMAX ? j : 0] : (j == NMAX ? rhs : 0.0);
+            }
+            bcast4(v[0], v[1], v[2], v[3], pm, u[0], u[1], u[2], u[3]);
+#pragma clang loop unroll(full)
+            for (int t = 0; t < 4; ++t) {
+              const int j = 4 * g + t;
+              if (j > k && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
+              if (j == NMAX) rhs = fma(-l, u[t], rhs);
+            }
+          }
         }
       }
+      MCPX_STAMP(1);
       if (singular) {
         status = 1;
         break;
@@ -255,6 +328,7 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
         }
       }
 
+      MCPX_STAMP(2);
       // ---- fraction-to-the-boundary line search (:93-100, :127-138) -----
       const bool ry = ln >= n && ln < n + m;
       const bool rs = ln >= n + m && ln < N;
@@ -288,6 +362,7 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       if (rx || rs) z = z + as * dz;
       if (ry) z = z + ay * dz;
       kkt = kkt_step;  // :107
+      MCPX_STAMP(3);
       ++inner;         // :108
       ++newton;
     }
@@ -307,6 +382,10 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
     const uint64_t act = ballot(ry && z > zs[min(lane + m, 63)]);
     if (lane == 0) args.active_mask[inst] = act >> n;
   }
+#if MCPX_STAMPS
+  if (lane == 0 && args.stamps)
+    for (int i = 0; i < 4; ++i) args.stamps[inst * 4 + i] = st_acc[i];
+#endif
   if (lane == 0) {
     args.kkt_error[inst] = kkt;
     args.eps[inst] = eps;

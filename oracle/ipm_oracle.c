@@ -28,6 +28,11 @@
  *    failure (the UMFPACK "singular" retcode of src/solver.jl:84);
  *    elimination a_ij ← fma(−l_i, u_j, a_ij) with l_i = a_ik / pivot;
  *    back substitution column-oriented with x_k = b_p / u_pk;
+ *  - linear_solver = MCPX_LINSOLVE_REDUCED (default) first eliminates the
+ *    slack block exactly: w_k = y_k + tol (the ∂F_C/∂s diagonal entry),
+ *    d_k = s_k / w_k added to the (H_k, y_k) diagonal entry after its tol,
+ *    rhs_Hk = (−F_Hk) − (F_Ck / w_k); the (n+m) system is solved by the LU
+ *    above and δs_k = fma(−s_k, δy_k, −F_Ck) / w_k;
  *    (UMFPACK itself, LinearSolve 2.38 UMFPACKFactorization, is a third-party
  *    sparse LU not present here: this dense LU replaces it, results differ in
  *    rounding only);
@@ -59,7 +64,8 @@ int oracle_build_tables(const mcpx_params* p, oracle_tables* t) {
   if (!(p->tol > 0) || !(p->min_stepsize > 0) || !(p->decay > 0 && p->decay < 1) ||
       !(p->tau == p->tau) || !(p->tightening_rate == p->tightening_rate) ||
       !(p->loosening_rate == p->loosening_rate) || p->max_inner_iters < 1 ||
-      p->max_outer_iters < 1)
+      p->max_outer_iters < 1 ||
+      (p->linear_solver != MCPX_LINSOLVE_REDUCED && p->linear_solver != MCPX_LINSOLVE_DENSE))
     return MCPX_EINVAL;
   if (p->max_inner_iters > MCPX_MAX_INNER_ITERS) return MCPX_EUNSUPPORTED;
   /* src/solver.jl:128-135: α = 1; while violated: if α < tol → NaN; α *= decay */
@@ -211,12 +217,13 @@ static int linesearch_exponent(const double* v, const double* d, int cnt, const 
 }
 
 typedef struct ws {
-  double *J, *row, *F, *b, *dz, *z;
+  double *J, *Jr, *row, *F, *b, *dz, *z;
   int *remaining, *step_of, *prow;
 } ws;
 
 static int ws_alloc(ws* w, int N) {
   w->J = (double*)malloc(sizeof(double) * (size_t)N * N);
+  w->Jr = (double*)malloc(sizeof(double) * (size_t)N * N);
   w->row = (double*)malloc(sizeof(double) * N);
   w->F = (double*)malloc(sizeof(double) * N);
   w->b = (double*)malloc(sizeof(double) * N);
@@ -225,10 +232,10 @@ static int ws_alloc(ws* w, int N) {
   w->remaining = (int*)malloc(sizeof(int) * N);
   w->step_of = (int*)malloc(sizeof(int) * N);
   w->prow = (int*)malloc(sizeof(int) * N);
-  return (w->J && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
+  return (w->J && w->Jr && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
 }
 static void ws_free(ws* w) {
-  free(w->J); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
+  free(w->J); free(w->Jr); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
   free(w->remaining); free(w->step_of); free(w->prow);
 }
 
@@ -258,9 +265,32 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
         w->b[i] = -w->F[i];
       }
       /* :83-88 */
-      if (lu_solve(N, w->J, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
-        status = MCPX_STATUS_FAILED;
-        break;
+      if (p->linear_solver == MCPX_LINSOLVE_DENSE) {
+        if (lu_solve(N, w->J, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
+          status = MCPX_STATUS_FAILED;
+          break;
+        }
+      } else {
+        /* exact elimination of the slack block, then LU of the (n+m) Schur complement */
+        const int Nr = n + m;
+        for (int k = 0; k < m; ++k) {
+          const int h = n + k, c = n + m + k;
+          const double wk = w->J[(size_t)c * N + c]; /* y_k + tol */
+          const double dk = z[c] / wk;               /* s_k / w_k */
+          w->J[(size_t)h * N + h] += dk;
+          w->b[h] = w->b[h] - (w->F[c] / wk);
+        }
+        for (int i = 0; i < Nr; ++i)
+          for (int j = 0; j < Nr; ++j) w->Jr[(size_t)i * Nr + j] = w->J[(size_t)i * N + j];
+        if (lu_solve(Nr, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
+          status = MCPX_STATUS_FAILED;
+          break;
+        }
+        for (int k = 0; k < m; ++k) {
+          const int c = n + m + k;
+          const double wk = w->J[(size_t)c * N + c];
+          w->dz[c] = fma(-z[c], w->dz[n + k], -w->F[c]) / wk;
+        }
       }
       /* :93-100 */
       const int es = linesearch_exponent(z + n + m, w->dz + n + m, m, t);

@@ -1,0 +1,72 @@
+// Diagnostic build: per-phase cycle shares of the IPM kernel (s_memtime stamps).
+// Not a timing build — read the shares, not the absolute time.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -DMCPX_STAMPS=1 \
+//          tools/phase_profile.hip mcp_amd/csrc/mcpx_api.cpp -o tools/phase_profile
+#include "../mcp_amd/csrc/ipm_kernel.hip"
+
+#include <cstdio>
+#include <cstring>
+#include <cmath>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 32, m = argc > 2 ? atoi(argv[2]) : 16;
+  const int B = argc > 3 ? atoi(argv[3]) : 16384;
+  const int p = n * n + m * n + m + n;
+  std::mt19937_64 g(7);
+  std::normal_distribution<double> nd;
+  std::vector<double> th((size_t)B * p);
+  for (int b = 0; b < B; ++b) {
+    double* t = &th[(size_t)b * p];
+    std::vector<double> P(n * n);
+    for (auto& v : P) v = nd(g);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        double acc = 0;
+        for (int k = 0; k < n; ++k) acc += P[k * n + i] * P[k * n + j];
+        t[j * n + i] = acc;
+      }
+    for (int i = n * n; i < p; ++i) t[i] = nd(g);
+  }
+  mcpx_desc d{0, n, m, 0, B, p};
+  mcpx_params prm;
+  mcpx_default_params(&prm);
+  prm.tol = 1e-6;
+  double *dth, *x, *y, *s, *kkt, *eps;
+  int *outer, *status, *newton;
+  uint64_t* stamps;
+  (void)hipMalloc(&dth, th.size() * 8);
+  (void)hipMemcpy(dth, th.data(), th.size() * 8, hipMemcpyHostToDevice);
+  (void)hipMalloc(&x, (size_t)B * n * 8); (void)hipMalloc(&y, (size_t)B * m * 8); (void)hipMalloc(&s, (size_t)B * m * 8);
+  (void)hipMalloc(&kkt, B * 8); (void)hipMalloc(&eps, B * 8);
+  (void)hipMalloc(&outer, B * 4); (void)hipMalloc(&status, B * 4); (void)hipMalloc(&newton, B * 4);
+  (void)hipMalloc(&stamps, (size_t)B * 4 * 8);
+  mcpx::KernelArgs a;
+  int nmax = 0;
+  // reuse the ABI's parameter preparation through a normal call first (fills nothing here)
+  std::memset((void*)&a, 0, sizeof a);
+  a.theta = dth; a.theta_ld = p; a.x = x; a.y = y; a.s = s; a.kkt_error = kkt; a.eps = eps;
+  a.outer_iters = outer; a.status = status; a.newton_iters = newton; a.stamps = stamps;
+  a.n = n; a.m = m; a.max_inner = prm.max_inner_iters; a.max_outer = prm.max_outer_iters; a.tol = prm.tol;
+  a.decay = 0.5; a.c_tau = 1.0 - 0.995; a.n_trials = 15;
+  for (int k = 0; k <= prm.max_inner_iters; ++k) { a.tight[k] = 1 - exp(-0.1 * k); a.loose[k] = 1 + exp(-0.5 * k); }
+  const int N = n + 2 * m;
+  nmax = N <= 8 ? 8 : N <= 16 ? 16 : N <= 32 ? 32 : 64;
+  for (int rep = 0; rep < 2; ++rep) {
+    (void)mcpx::launch_ipm(nmax, 0, a, B, 0, getenv("MCPX_GENERIC_KERNELS") == nullptr);
+    (void)hipDeviceSynchronize();
+  }
+  std::vector<uint64_t> st((size_t)B * 4);
+  std::vector<int> nw(B);
+  (void)hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(nw.data(), newton, B * 4, hipMemcpyDeviceToHost);
+  double tot[4] = {0, 0, 0, 0}, nsteps = 0;
+  for (int b = 0; b < B; ++b) { for (int i = 0; i < 4; ++i) tot[i] += st[(size_t)b * 4 + i]; nsteps += nw[b]; }
+  const double all = tot[0] + tot[1] + tot[2] + tot[3];
+  const char* nm[] = {"assemble+kkt", "LU+fwd", "backsub", "linesearch+update"};
+  printf("n=%d m=%d B=%d  mean newton %.2f  wave-cycles per Newton step %.0f\n", n, m, B, nsteps / B, all / nsteps);
+  for (int i = 0; i < 4; ++i) printf("  %-18s %5.1f%%  %8.0f cyc/step\n", nm[i], 100 * tot[i] / all, tot[i] / nsteps);
+  return 0;
+}
