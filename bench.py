@@ -30,8 +30,15 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (AMD datasheet;
 
 
 def lu_flops(N: int) -> float:
-    """Algorithmic FLOPs of one Newton step's dense solve: 2N³/3 + 2N²."""
+    """FLOPs of one dense LU with partial pivoting + the two triangular solves of an
+    N-dim system: 2N³/3 + 2N²."""
     return 2.0 * N ** 3 / 3.0 + 2.0 * N ** 2
+
+
+def solve_dim(n: int, m: int, linear_solver: str) -> int:
+    """Dimension of the system the kernel factors per Newton step: n + m after the
+    exact slack elimination (default), n + 2m for the full dense LU."""
+    return n + m if linear_solver == "reduced" else n + 2 * m
 
 
 def parse():
@@ -45,23 +52,26 @@ def parse():
     ap.add_argument("--tol", type=float, default=1e-6)
     ap.add_argument("--sparsity", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-sample", type=int, default=8192, help="instances in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--linear-solver", default="reduced", choices=["reduced", "dense"])
+    ap.add_argument("--cpu-sample", type=int, default=32768, help="instances in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     return ap.parse_args()
 
 
-def cpu_baseline(theta_host: np.ndarray, n: int, m: int, tol: float, threads: int) -> dict:
+def cpu_baseline(theta_host: np.ndarray, n: int, m: int, tol: float, threads: int, ls: str) -> dict:
     """Times the C oracle (oracle/ipm_oracle.c, same algorithm) on host cores."""
     from oracle import coracle
 
     coracle.build()
-    coracle.solve_batch(0, n, m, theta_host[: min(64, len(theta_host))], tol=tol, nthreads=threads)  # warm
+    coracle.solve_batch(0, n, m, theta_host[: min(64, len(theta_host))], tol=tol, nthreads=threads,
+                        linear_solver=ls)  # warm
     t0 = time.perf_counter()
-    r = coracle.solve_batch(0, n, m, theta_host, tol=tol, nthreads=threads)
+    r = coracle.solve_batch(0, n, m, theta_host, tol=tol, nthreads=threads, linear_solver=ls)
     dt = time.perf_counter() - t0
     return dict(value=len(theta_host) / dt, unit="solves/s", cores=threads, kind="port",
                 sample=f"{len(theta_host)} instances of the same workload (first {len(theta_host)} θ of rank 0), "
-                       f"C oracle (oracle/ipm_oracle.c) on {threads} host threads, {dt:.2f} s wall",
+                       f"C oracle (oracle/ipm_oracle.c, same algorithm and linear solver) on {threads} host threads, "
+                       f"{dt:.2f} s wall = {dt * threads:.1f} thread-s",
                 newton_mean=float(r["newton_iters"].mean()))
 
 
@@ -103,7 +113,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def step():
-        solve_batch_device(0, n, m, theta, out, tol=a.tol, stream=stream)
+        solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
         if world > 1:
             dist.all_gather_into_tensor(grec, rec)
             dist.all_gather_into_tensor(girec, irec)
@@ -118,7 +128,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         ev[i][0].record(stream)
-        solve_batch_device(0, n, m, theta, out, tol=a.tol, stream=stream)
+        solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
         ev[i][1].record(stream)
         if world > 1:
             dist.all_gather_into_tensor(grec, rec)
@@ -139,7 +149,8 @@ def main():
         newton, solved = float(s[0]), float(s[1]) / world
 
     if rank == 0:
-        flops_launch = newton / world * lu_flops(N)  # per-launch (per GPU) algorithmic FLOPs
+        NS = solve_dim(n, m, a.linear_solver)
+        flops_launch = newton / world * lu_flops(NS)  # per-launch (per GPU) algorithmic FLOPs
         achieved = flops_launch / (kern_ms * 1e-3) / 1e12
         res = {
             "metric": METRIC,
@@ -157,7 +168,8 @@ def main():
                     f"{a.seed}+rank, generated in HBM)",
             "config": {"workload": f"BASELINE C3: random dense QP-KKT n={n} m={m} (KKT dim {N}), fp64, "
                                    f"{B} instances per GPU, tol={a.tol:g}",
-                       "n": n, "m": m, "kkt_dim": N, "batch_per_gpu": B, "global_batch": B * world,
+                       "n": n, "m": m, "kkt_dim": N, "linear_solver": a.linear_solver, "solve_dim": NS,
+                       "batch_per_gpu": B, "global_batch": B * world,
                        "sparsity": a.sparsity,
                        "parallelism": f"dp{world} (instance shards, RCCL all-gather of results)" if world > 1
                        else "dp1"},
@@ -165,14 +177,18 @@ def main():
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
                          "kernel": "ipm_solve_kernel", "kernel_ms": kern_ms,
                          "flops_per_launch": flops_launch,
-                         "note": "FP64 dense-LU FLOPs 2N^3/3+2N^2 per Newton step x the run's own Newton "
-                                 "counts / HIP-event kernel time; FP64 vector and matrix peaks are equal on MI355X"},
+                         "dense_kkt_equiv_tflops": newton / world * lu_flops(N) / (kern_ms * 1e-3) / 1e12,
+                         "note": f"FP64 LU FLOPs 2N^3/3+2N^2 of the system actually factored (N={NS}, "
+                                 f"{a.linear_solver}) per Newton step x the run's own Newton counts / HIP-event "
+                                 f"kernel time; dense_kkt_equiv_tflops prices the same run at the full KKT dim "
+                                 f"{N} (SURVEY.md §8d formula); FP64 vector and matrix peaks are equal on MI355X"},
             "newton_iters_mean": newton / (B * world),
             "success_rate": solved,
         }
         if world == 1 and a.cpu_sample > 0:
             th = int(a.cpu_threads) or min(16, os.cpu_count() or 1)
-            res["cpu_baseline"] = cpu_baseline(theta[: a.cpu_sample].cpu().numpy(), n, m, a.tol, th)
+            res["cpu_baseline"] = cpu_baseline(theta[: a.cpu_sample].cpu().numpy(), n, m, a.tol, th,
+                                               a.linear_solver)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -19,8 +19,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmcpx.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("ipm_kernel.hip", "mcpx_api.cpp")]
-DEPS = SOURCES + [os.path.join(CSRC, "ipm_kernel.h"), os.path.join(ROOT, "include", "mcpx.h")]
+SOURCES = [os.path.join(CSRC, f) for f in (
+    "ipm_inst_red_qp.hip", "ipm_inst_spec.hip", "ipm_inst_red_aff.hip", "ipm_inst_dense_qp.hip",
+    "ipm_inst_dense_aff.hip", "mcpx_api.cpp")]
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("ipm_kernel.h", "ipm_kernel_impl.hpp", "bcast_group.inc")] + [
+    os.path.join(ROOT, "include", "mcpx.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
@@ -37,15 +40,21 @@ def _stale() -> bool:
 def build(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
     if not force and not _stale():
         return LIB
-    objs = []
     t0 = time.time()
-    for src in SOURCES:
+    objs, procs = [], []
+    jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 1)
+    for src in SOURCES:  # one hipcc per translation unit, `jobs` at a time
         obj = os.path.join(CSRC, os.path.basename(src) + ".o")
         cmd = [HIPCC, *FLAGS, *extra_flags, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        procs.append(subprocess.Popen(cmd))
         objs.append(obj)
+        while sum(p.poll() is None for p in procs) >= jobs:
+            time.sleep(0.2)
+    for p, src in zip(procs, SOURCES):
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, f"hipcc {src}")
     tmp = LIB + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
     os.replace(tmp, LIB)

@@ -28,6 +28,8 @@ struct KernelArgs {
   uint64_t* stamps;  // diagnostic builds only (MCPX_STAMPS); NULL otherwise
   int32_t trace_len;
   int32_t n, m;
+  int32_t family;   // MCPX_FAMILY_*
+  int32_t reduced;  // 1: MCPX_LINSOLVE_REDUCED, 0: MCPX_LINSOLVE_DENSE
   int32_t max_inner, max_outer;
   int32_t n_trials;  // line-search trials e = 0 .. n_trials-1 (α_e = decayᵉ)
   double tol;
@@ -37,10 +39,15 @@ struct KernelArgs {
   double loose[MCPX_MAX_INNER_ITERS + 1];  // 1 + exp(−l·k), src/solver.jl:113
 };
 
-// Launches the register-resident solver: one 64-lane wave (= one workgroup)
-// per instance.  nmax ∈ {8,16,32,64} ≥ n + 2m; family = MCPX_FAMILY_*.
-// allow_specialized: use a compile-time-(n, m) kernel when one matches.
-hipError_t launch_ipm(int nmax, int family, const KernelArgs& args, int64_t batch, hipStream_t stream,
-                      bool allow_specialized);
+// Launchers of the register-resident solver: one 64-lane wave (= one
+// workgroup) per instance.  nmax ∈ {8,16,24,32,48,64} ≥ the linear-system dimension
+// (n + m reduced, n + 2m dense).  Each returns hipErrorNotFound /
+// hipErrorInvalidValue when it has no matching kernel.
+hipError_t launch_ipm_spec(int family, bool reduced, int n, int m, const KernelArgs& a, int64_t batch,
+                           hipStream_t st);
+hipError_t launch_ipm_red_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
+hipError_t launch_ipm_red_aff(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
+hipError_t launch_ipm_dense_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
+hipError_t launch_ipm_dense_aff(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 
 }  // namespace mcpx

@@ -1,0 +1,482 @@
+// ipm_kernel_impl.hpp — gfx950 (CDNA4) kernel templates of the batched interior-point
+// MCP solver.  Instantiated by ipm_inst_*.hip (one translation unit per kernel
+// group so the build compiles them in parallel).
+//
+// One 64-lane wavefront solves one MCP instance end to end: the whole
+// ϵ-continuation / Newton loop of the reference, src/solver.jl:64-121, runs on
+// the device with no host round trip.  Lane i owns row i of the Newton system
+// (∇F + tol·I) δz = −F (src/mcp.jl:76-120, src/solver.jl:81-82):
+//
+//  * RED (default, MCPX_LINSOLVE_REDUCED): the slack block is eliminated
+//    exactly first — ∂(s⊙y − ϵ)/∂s = Y + tol·I is diagonal for every MCP of the
+//    reference's form — so lanes [0, n) hold x-rows (G) and lanes [n, n+m)
+//    hold y-rows (H − s) together with y_k and s_k; the system is (n+m)-dim.
+//  * DENSE (MCPX_LINSOLVE_DENSE): lanes [0, n+2m) hold the rows of the full
+//    system, z = [x; y; s] one entry per lane.
+//
+// The Newton system (src/solver.jl:81-90, UMFPACK in the reference) is solved
+// by a register-resident dense LU with partial pivoting on the augmented
+// matrix [K | rhs]: rows stay in their lanes (NMAX fp64 VGPRs each); the pivot
+// search is a 32-bit DPP max over the high word of |a_ik| with exact two-phase
+// tie resolution on the low word; the pivot row is broadcast through SGPRs
+// (EXEC-masked v_readfirstlane, bcast_group.inc, ≤16 columns per EXEC switch)
+// and every remaining lane eliminates with v_fma_f64.  Back substitution is
+// column-oriented.  The fraction-to-the-boundary line search
+// (src/solver.jl:127-138) evaluates every trial step α = decayᵉ at once (one
+// ballot per e) and takes the first all-clear e.
+//
+// Arithmetic is the contract of oracle/ipm_oracle.c (same op order, explicit
+// fma, -ffp-contract=off), so results are bit-identical to the CPU oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ipm_kernel.h"
+
+// Diagnostic phase stamps (tools/phase_profile.hip builds with MCPX_STAMPS=1;
+// the product build compiles them away).
+#ifndef MCPX_STAMPS
+#define MCPX_STAMPS 0
+#endif
+#if MCPX_STAMPS
+#define MCPX_STAMP(i)                                 \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += t_ - st_last;                        \
+    st_last = t_;                                     \
+  } while (0)
+#else
+#define MCPX_STAMP(i) \
+  do {                \
+  } while (0)
+#endif
+
+namespace mcpx {
+
+namespace {
+
+#include "bcast_group.inc"
+
+__device__ __forceinline__ double bcast(double v, int src) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ int lowest_lane(uint64_t mask) { return __ffsll((unsigned long long)mask) - 1; }
+
+// Hides a uniform value from the optimiser for one loop iteration so that the
+// ~3·NMAX uniform predicates derived from it (j < n, k < N, …) are recomputed
+// where used instead of being hoisted out of the Newton loop and kept live in
+// SGPRs (which spills them into VGPR lanes).
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+// Same for an offset on the θ pointer and for the lane index: keeps the NMAX
+// per-lane θ addresses of the Jacobian assembly from being hoisted out of the
+// Newton loop (they would occupy 2·NMAX registers for the whole solve).
+__device__ __forceinline__ int64_t opaque64(int64_t v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+__device__ __forceinline__ int opaque_lane(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Wave-wide max of an unsigned 32-bit key, result uniform.  DPP row_shr
+// 1/2/4/8 then row_bcast 15/31 (GFX9 DPP; 0 is the identity for `max`).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Exact wave max of non-negative, non-NaN doubles (bit patterns are monotone).
+__device__ __forceinline__ double wave_max_nonneg(double v) {
+  const uint32_t hi = (uint32_t)__double2hiint(v);
+  const uint32_t lo = (uint32_t)__double2loint(v);
+  const uint32_t mhi = wave_max_u32(hi);
+  const uint32_t mlo = wave_max_u32(hi == mhi ? lo : 0u);
+  return __hiloint2double((int)mhi, (int)mlo);
+}
+
+// NaN-propagating max (Julia `max`, as in norm(F, Inf), src/solver.jl:107)
+__device__ __forceinline__ double max_nan(double a, double b) { return (a != a || b != b) ? a + b : fmax(a, b); }
+
+// Row `lane` of F and of ∇F_z + tol·I (DENSE) or of the slack-eliminated
+// system (RED), src/mcp.jl:72-120.  `zs` is the wave's copy of z in LDS:
+// zs[j] = x_j (j < n), zs[n+q] = y_q, and for DENSE zs[n+m+q] = s_q.
+// `s_own` is s_k of a RED y-row.  Same op order as family_row() and the slack
+// elimination of oracle/ipm_oracle.c.  Every lane streams its row of θ
+// through one per-lane base pointer and stride per column block (no
+// per-column branches); lanes that read nothing in a block get stride 0 on a
+// valid address and a masked value.
+template <int NMAX, int FAMILY, bool RED, bool CT>
+__device__ __forceinline__ void assemble_row(const double* __restrict__ th, const double* zs, int lane, int n,
+                                             int m, double eps, double tol, double s_own, double (&a)[NMAX],
+                                             double& F, double& Fc, double& rhs, double& w) {
+  const int N = RED ? n + m : n + 2 * m;
+  const bool rg = lane < n;                           // G rows
+  const bool rh = lane >= n && lane < n + m;          // H − s rows
+  const bool rc = !RED && lane >= n + m && lane < N;  // s⊙y − ϵ rows (DENSE only)
+  const int kh = lane - n;                            // H row index
+  const int kc = lane - n - m;                        // complementarity index (DENSE)
+  const int nn = n * n, nm = n * m, mm = m * m;
+  // x-column block: G rows read M[i,:] / P[i,:], H rows A[k,:] / R[k,:]
+  const double* px = th;
+  int sx = 0;
+  if (rg) { px = th + lane; sx = n; }
+  if (rh) { px = th + (FAMILY == 0 ? nn : nn + nm) + kh; sx = m; }
+  // y-column block: QP G rows read A[:,i] (contiguous); affine G rows Q[i,:], H rows S[k,:]
+  const double* py = th;
+  int sy = 0;
+  if (FAMILY == 0) {
+    if (rg) { py = th + nn + lane * m; sy = 1; }
+  } else {
+    if (rg) { py = th + nn + lane; sy = n; }
+    if (rh) { py = th + nn + 2 * nm + kh; sy = m; }
+  }
+  const bool use_x = rg || rh;
+  const bool use_y = (FAMILY == 0) ? rg : (rg || rh);
+  // s_k / y_k of this row's complementarity pair
+  const double s_k = RED ? s_own : zs[min(n + m + (rc ? kc : max(kh, 0)), 63)];
+  const double y_k = zs[min(n + (RED ? max(kh, 0) : max(kc, 0)), 63)];
+  // RED: pivot w_k = y_k + tol of the eliminated δs_k and the Schur term d_k = s_k / w_k
+  w = y_k + tol;
+  const double d = (RED && rh) ? s_k / w : 0.0;
+  double acc = 0.0;
+  if constexpr (CT) {
+    // Compile-time (n, m): branch-free over columns, so the compiler batches
+    // the θ loads of neighbouring columns.  Every lane issues one load per
+    // column from a valid address and masks the value.
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      const int q = j - n, qs = q - m;  // column class, folded at compile time
+      const bool cx = q < 0;
+      const bool cy = q >= 0 && q < m;
+      const bool cs = !RED && qs >= 0 && qs < m;
+      const double* pa = cx ? px + j * sx : (cy ? py + q * sy : th);
+      const double t = *pa;
+      const double zj = zs[j];
+      double v = 0.0;
+      v = (cx && use_x) ? t : v;
+      v = (cy && use_y) ? ((FAMILY == 0) ? -t : t) : v;
+      v = (cy && rc && q == kc) ? s_k : v;   // ∂(s⊙y)/∂y = diag(s)
+      v = (cs && rh && qs == kh) ? -1.0 : v; // ∂(H − s)/∂s = −I
+      v = (cs && rc && qs == kc) ? y_k : v;  // ∂(s⊙y)/∂s = diag(y)
+      const double na = fma(v, zj, acc);
+      acc = (cx || (cy && use_y)) ? na : acc;
+      if (j == lane) {
+        v += tol;                 // src/solver.jl:81 ∇F + tol*I
+        if (RED && rh) v += d;    // + s_k / w_k from the slack elimination
+      }
+      a[j] = v;
+      if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // bound the load look-ahead
+    }
+  } else {
+    // Runtime (n, m): per-column uniform branches keep the register pressure
+    // of the generic kernels low (a branch-free stream raises it by ~60 VGPRs).
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) {
+      double v = 0.0;
+      if (j < n) {  // x columns
+        const double t = px[j * sx];
+        v = use_x ? t : 0.0;
+        acc = fma(v, zs[j], acc);
+      } else if (j < n + m) {  // y columns
+        const int q = j - n;
+        const double t = py[q * sy];
+        if (use_y) v = (FAMILY == 0) ? -t : t;
+        if (rc && q == kc) v = s_k;  // ∂(s⊙y)/∂y = diag(s)
+        const double na = fma(v, zs[j], acc);
+        acc = use_y ? na : acc;
+      } else if (!RED && j < N) {  // s columns (DENSE)
+        const int q = j - n - m;
+        if (rh && q == kh) v = -1.0;  // ∂(H − s)/∂s = −I
+        if (rc && q == kc) v = y_k;   // ∂(s⊙y)/∂s = diag(y)
+      }
+      if (j == lane) {
+        v += tol;               // src/solver.jl:81 ∇F + tol*I
+        if (RED && rh) v += d;  // + s_k / w_k from the slack elimination
+      }
+      a[j] = v;
+      if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  F = 0.0;
+  if (FAMILY == 0) {
+    if (rg) F = acc - th[nn + nm + m + lane];           // G = Mx − Aᵀy − ϕ
+    if (rh) F = (acc - th[nn + nm + kh]) - s_k;         // H − s = (Ax − b) − s
+  } else {
+    if (rg) F = acc + th[nn + 2 * nm + mm + lane];      // G = Px + Qy + g
+    if (rh) F = (acc + th[nn + 2 * nm + mm + n + kh]) - s_k;
+  }
+  Fc = 0.0;
+  if (RED) {
+    if (rh) {  // exact elimination of δs_k: rhs_H = −F_H − F_C / w_k
+      Fc = s_k * y_k - eps;
+      rhs = (-F) - (Fc / w);
+    } else {
+      rhs = -F;
+    }
+  } else {
+    if (rc) F = s_k * y_k - eps;  // s⊙y − ϵ
+    rhs = -F;
+  }
+}
+
+// Dense LU with partial pivoting of the rows held in lanes [0, N) plus the
+// augmented right-hand side, then column-oriented back substitution.  On
+// success returns true and the solution entry of column `ln` in dz; returns
+// false if a pivot is exactly 0.
+template <int NMAX>
+__device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int N, int ln, double& dz) {
+  uint64_t rem = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
+  int my_step = 1 << 30;  // LU step at which this row became a pivot row
+  int pk = 0;             // lane k: pivot row of step k
+  bool singular = false;
+#pragma clang loop unroll(full)
+  for (int k = 0; k < NMAX; ++k) {
+    if (k >= N || singular) continue;  // uniform; no `break` so the loop fully unrolls
+    const double ak = a[k];
+    const double av = fabs(ak);
+    const bool valid = ((rem >> ln) & 1ull) && !(av != av);
+    const uint32_t khi = valid ? (uint32_t)__double2hiint(av) + 1u : 0u;
+    const uint32_t mhi = wave_max_u32(khi);
+    int p;
+    if (mhi == 0u) {
+      p = lowest_lane(rem);  // every remaining entry is NaN
+    } else {
+      const uint64_t cand = ballot(khi == mhi);
+      if (__popcll(cand) == 1) {
+        p = lowest_lane(cand);
+      } else {  // exact tie-break on the low word, lowest lane wins
+        const uint32_t klo = (khi == mhi) ? (uint32_t)__double2loint(av) : 0u;
+        const uint32_t mlo = wave_max_u32(klo);
+        p = lowest_lane(ballot(khi == mhi && klo == mlo));
+      }
+    }
+    const double piv = bcast(ak, p);
+    if (piv == 0.0) {  // singular: the failed linear solve of src/solver.jl:84-88
+      singular = true;
+      continue;
+    }
+    rem &= ~(1ull << p);
+    if (ln == p) my_step = k;
+    if (ln == k) pk = p;
+    if ((rem >> ln) & 1ull) {
+      const double l = ak / piv;
+      const uint64_t pm = 1ull << p;
+      constexpr int G = 16;  // columns per EXEC-masked broadcast
+      // columns k+1 .. NMAX-1 and the right-hand side (index NMAX)
+#pragma clang loop unroll(full)
+      for (int g = 0; g <= NMAX / G; ++g) {
+        const int lo = max(G * g, k + 1);        // static after unrolling
+        const int hi = min(G * g + G, NMAX + 1);  // exclusive
+        if (lo >= hi) continue;
+        const int cnt = hi - lo;  // 1..16
+        double v[16], u[16];
+#pragma clang loop unroll(full)
+        for (int t = 0; t < 16; ++t) {
+          const int j = lo + t;
+          v[t] = (t < cnt) ? ((j < NMAX) ? a[j < NMAX ? j : 0] : rhs) : 0.0;
+        }
+        bcast_n(cnt, v, pm, u);
+#pragma clang loop unroll(full)
+        for (int t = 0; t < 16; ++t) {
+          const int j = lo + t;
+          if (t < cnt && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
+          if (t < cnt && j == NMAX) rhs = fma(-l, u[t], rhs);
+        }
+      }
+    }
+  }
+  if (singular) return false;
+  dz = 0.0;
+#pragma clang loop unroll(full)
+  for (int k = NMAX - 1; k >= 0; --k) {
+    if (k < N) {
+      const int p = __builtin_amdgcn_readlane(pk, k);
+      const double t = rhs / a[k];
+      const double xk = bcast(t, p);
+      if (ln == k) dz = xk;
+      if (my_step < k) rhs = fma(-a[k], xk, rhs);
+    }
+  }
+  return true;
+}
+
+}  // namespace
+
+// NC, MC > 0: compile-time (n, m) specialisation; 0: runtime n, m.
+// RED: slack-eliminated (n+m)-dim system; otherwise the full (n+2m)-dim one.
+template <int NMAX, int FAMILY, int NC, int MC, bool RED>
+__global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
+  __shared__ double zs[64];
+  const int lane = threadIdx.x;
+  const int64_t inst = blockIdx.x;
+  const int n0 = NC ? NC : args.n, m0 = MC ? MC : args.m;
+  const double* const th0 = args.theta + inst * args.theta_ld;
+  const double tol = args.tol;
+
+  // src/solver.jl:39-41, 64-66: x₀ = 0, y₀ = 1, s₀ = 1 unless warm-started.
+  // DENSE: z = [x; y; s] one per lane.  RED: lanes [0,n) x, [n,n+m) (y, s).
+  double z = 0.0, s = 1.0;
+  {
+    const int n = n0, m = m0;
+    if (lane < n) z = args.x0 ? args.x0[inst * n + lane] : 0.0;
+    if (lane >= n && lane < n + m) {
+      z = args.y0 ? args.y0[inst * m + (lane - n)] : 1.0;
+      if (RED) s = args.s0 ? args.s0[inst * m + (lane - n)] : 1.0;
+    }
+    if (!RED && lane >= n + m && lane < n + 2 * m) z = args.s0 ? args.s0[inst * m + (lane - n - m)] : 1.0;
+  }
+
+  double eps = 1.0;                    // :67
+  double kkt = __builtin_huge_val();   // :68
+  int status = 0;                      // :69
+  int outer = 1;                       // :70
+  int newton = 0;
+#if MCPX_STAMPS
+  uint64_t st_acc[4] = {0, 0, 0, 0};
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
+
+  while (kkt > tol && eps > tol && outer < args.max_outer) {  // :71
+    int inner = 1;   // :72
+    status = 0;      // :73
+    while (kkt > eps && inner < args.max_inner) {  // :75
+      const int n = NC ? NC : opaque(n0), m = MC ? MC : opaque(m0);
+      const int NS = RED ? n + m : n + 2 * m;             // rows of the linear system
+      const double* __restrict__ th = th0 + opaque64(0);  // stays a global pointer
+      const int ln = opaque_lane(lane);
+      // ---- F!, ∇F_z! (:79-81) --------------------------------------------
+      __syncthreads();
+      zs[ln] = z;
+      __syncthreads();
+      double a[NMAX];
+      double F, Fc, rhs, w;
+      assemble_row<NMAX, FAMILY, RED, (NC > 0)>(th, zs, ln, n, m, eps, tol, s, a, F, Fc, rhs, w);
+      // ‖F‖∞ with NaN propagation (:107), taken now, committed after the step
+      const bool rh = ln >= n && ln < n + m;
+      double aF = (ln < NS) ? fabs(F) : 0.0;
+      if (RED && rh) aF = max_nan(aF, fabs(Fc));
+      const bool any_nan = ballot(aF != aF) != 0ull;
+      const double kkt_step = any_nan ? __builtin_nan("") : wave_max_nonneg(aF);
+      MCPX_STAMP(0);
+
+      // ---- dense LU with partial pivoting (:81-83) -----------------------
+      double dz = 0.0;
+      const bool ok = lu_solve_rows<NMAX>(a, rhs, NS, ln, dz);
+      MCPX_STAMP(1);
+      if (!ok) {
+        status = 1;
+        break;
+      }
+      double ds = 0.0;
+      if (RED && rh) ds = fma(-s, dz, -Fc) / w;  // δs_k = (−F_Ck − s_k δy_k) / w_k
+      MCPX_STAMP(2);
+
+      // ---- fraction-to-the-boundary line search (:93-100, :127-138) -----
+      const bool ry = rh;
+      const bool rs = RED ? rh : (ln >= n + m && ln < NS);
+      const double sv = RED ? s : z, sd = RED ? ds : dz;  // this lane's s entry and δs
+      const double cvy = args.c_tau * z, cvs = args.c_tau * sv;
+      uint64_t vs = 0ull, vy = 0ull;
+      double alpha = 1.0;
+      for (int e = 0; e < args.n_trials; ++e) {
+        const double ty = alpha * dz, ts = alpha * sd;
+        const double ly = z + ty, ls = sv + ts;
+        if (ballot(rs && ls < cvs)) vs |= 1ull << e;
+        if (ballot(ry && ly < cvy)) vy |= 1ull << e;
+        alpha *= args.decay;
+      }
+      const int es = (~vs) ? lowest_lane(~vs) : 64;
+      const int ey = (~vy) ? lowest_lane(~vy) : 64;
+      if (es >= args.n_trials || ey >= args.n_trials) {  // α = NaN
+        status = 1;
+        break;
+      }
+      double as = 1.0, ay = 1.0;
+      for (int e = 0; e < es; ++e) as *= args.decay;
+      for (int e = 0; e < ey; ++e) ay *= args.decay;
+      if (args.alpha_trace && newton < args.trace_len && ln == 0) {
+        uint8_t* tr = args.alpha_trace + ((size_t)inst * args.trace_len + newton) * 2;
+        tr[0] = (uint8_t)es;
+        tr[1] = (uint8_t)ey;
+      }
+      // ---- update (:103-105; x moves with α_s) --------------------------
+      const bool rx = ln < n;
+      if (RED) {
+        if (rx) z = z + as * dz;
+        if (rh) {
+          s = s + as * ds;
+          z = z + ay * dz;
+        }
+      } else {
+        if (rx || rs) z = z + as * dz;
+        if (ry) z = z + ay * dz;
+      }
+      kkt = kkt_step;  // :107
+      MCPX_STAMP(3);
+      ++inner;         // :108
+      ++newton;
+    }
+    eps *= (status == 0) ? args.tight[inner] : args.loose[inner];  // :111-113
+    ++outer;                                                        // :114
+  }
+  if (outer == args.max_outer) status = 1;  // :117-119
+
+  // ---- outputs (:121) -----------------------------------------------------
+  const int n = n0, m = m0;
+  const bool rx = lane < n, ry = lane >= n && lane < n + m;
+  if (rx) args.x[inst * n + lane] = z;
+  if (ry) args.y[inst * m + (lane - n)] = z;
+  if (RED) {
+    if (ry) args.s[inst * m + (lane - n)] = s;
+    if (args.active_mask) {
+      const uint64_t act = ballot(ry && z > s);
+      if (lane == 0) args.active_mask[inst] = act >> n;
+    }
+  } else {
+    const bool rs = lane >= n + m && lane < n + 2 * m;
+    if (rs) args.s[inst * m + (lane - n - m)] = z;
+    if (args.active_mask) {
+      __syncthreads();
+      zs[lane] = z;
+      __syncthreads();
+      const uint64_t act = ballot(ry && z > zs[min(lane + m, 63)]);
+      if (lane == 0) args.active_mask[inst] = act >> n;
+    }
+  }
+#if MCPX_STAMPS
+  if (lane == 0 && args.stamps)
+    for (int i = 0; i < 4; ++i) args.stamps[inst * 4 + i] = st_acc[i];
+#endif
+  if (lane == 0) {
+    args.kkt_error[inst] = kkt;
+    args.eps[inst] = eps;
+    args.outer_iters[inst] = outer;
+    args.status[inst] = status;
+    if (args.newton_iters) args.newton_iters[inst] = newton;
+  }
+}
+
+// Launch helper used by the instantiation units.
+template <int NMAX, int FAMILY, int NC, int MC, bool RED>
+hipError_t launch_one(const KernelArgs& args, int64_t batch, hipStream_t stream) {
+  hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, RED>), dim3((unsigned)batch), dim3(64), 0, stream,
+                     args);
+  return hipGetLastError();
+}
+
+}  // namespace mcpx

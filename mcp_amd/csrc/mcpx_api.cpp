@@ -57,11 +57,10 @@ bool specialized_enabled() {
   return !(e && e[0] == '1');
 }
 
+// Register-row width of the runtime-(n, m) kernels: smallest compiled width ≥ N.
 int pick_nmax(int N) {
-  if (N <= 8) return 8;
-  if (N <= 16) return 16;
-  if (N <= 32) return 32;
-  if (N <= 64) return 64;
+  for (int w : {8, 16, 24, 32, 48, 64})
+    if (N <= w) return w;
   return -1;
 }
 
@@ -73,9 +72,14 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   if (d->n + d->m < 1) return fail(MCPX_EINVAL, "empty problem (n = m = 0)");
   if (d->batch < 0) return fail(MCPX_EINVAL, "negative batch");
   if (d->theta_ld < pd) return fail(MCPX_EINVAL, "theta_ld %lld < parameter dimension %lld", (long long)d->theta_ld, (long long)pd);
-  const int N = d->n + 2 * d->m;
+  if (p->linear_solver != MCPX_LINSOLVE_REDUCED && p->linear_solver != MCPX_LINSOLVE_DENSE)
+    return fail(MCPX_EINVAL, "unknown linear_solver %d", p->linear_solver);
+  const bool red = p->linear_solver == MCPX_LINSOLVE_REDUCED;
+  const int N = red ? d->n + d->m : d->n + 2 * d->m;
   *nmax = pick_nmax(N);
-  if (*nmax < 0) return fail(MCPX_EUNSUPPORTED, "KKT dimension %d > %d not supported by the register-resident kernel", N, MCPX_MAX_KKT_DIM);
+  if (*nmax < 0)
+    return fail(MCPX_EUNSUPPORTED, "linear-system dimension %d (%s) > %d not supported by the register-resident kernel",
+                N, red ? "n+m" : "n+2m", MCPX_MAX_KKT_DIM);
   if (!(p->tol > 0) || !(p->min_stepsize > 0) || !(p->decay > 0 && p->decay < 1) || std::isnan(p->tau) ||
       std::isnan(p->tightening_rate) || std::isnan(p->loosening_rate) || p->max_inner_iters < 1 ||
       p->max_outer_iters < 1)
@@ -85,6 +89,8 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   std::memset(a, 0, sizeof *a);
   a->n = d->n;
   a->m = d->m;
+  a->reduced = red ? 1 : 0;
+  a->family = d->family;
   a->theta_ld = d->theta_ld;
   a->max_inner = p->max_inner_iters;
   a->max_outer = p->max_outer_iters;
@@ -108,6 +114,19 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   return MCPX_OK;
 }
 
+// Picks the kernel: a compile-time-(n, m) specialisation when one exists (and
+// MCPX_GENERIC_KERNELS is not set), else the runtime-(n, m) kernel for nmax.
+hipError_t launch(int nmax, const mcpx::KernelArgs& a, int64_t nb, hipStream_t st) {
+  if (specialized_enabled()) {
+    const hipError_t e = mcpx::launch_ipm_spec(a.family, a.reduced != 0, a.n, a.m, a, nb, st);
+    if (e != hipErrorNotFound) return e;
+  }
+  if (a.reduced) return a.family == MCPX_FAMILY_QP ? mcpx::launch_ipm_red_qp(nmax, a, nb, st)
+                                                   : mcpx::launch_ipm_red_aff(nmax, a, nb, st);
+  return a.family == MCPX_FAMILY_QP ? mcpx::launch_ipm_dense_qp(nmax, a, nb, st)
+                                    : mcpx::launch_ipm_dense_aff(nmax, a, nb, st);
+}
+
 int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                   const double* s0, const mcpx_out* o, mcpx::KernelArgs a, int nmax, hipStream_t st) {
   const int64_t CH = (int64_t)1 << 30;
@@ -129,7 +148,7 @@ int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, con
     a.active_mask = o->active_mask ? o->active_mask + b0 : nullptr;
     a.alpha_trace = (o->alpha_trace && o->trace_len > 0) ? o->alpha_trace + b0 * (int64_t)o->trace_len * 2 : nullptr;
     a.trace_len = o->alpha_trace ? o->trace_len : 0;
-    HIP_TRY(mcpx::launch_ipm(nmax, d->family, a, nb, st, specialized_enabled()));
+    HIP_TRY(launch(nmax, a, nb, st));
   }
   return MCPX_OK;
 }

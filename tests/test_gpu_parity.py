@@ -55,9 +55,12 @@ def _params_from(d):
     return kw
 
 
+LS = ["reduced", "dense"]
+
+
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(HERE, "golden", "*.npz"))),
                          ids=lambda p: os.path.basename(p)[:-4])
-@pytest.mark.parametrize("variant", ["specialized", "generic"])
+@pytest.mark.parametrize("variant", ["specialized", "generic"])  # MCPX_GENERIC_KERNELS A/B
 def test_golden(gpu, path, variant, monkeypatch):
     if variant == "generic":
         monkeypatch.setenv("MCPX_GENERIC_KERNELS", "1")
@@ -86,16 +89,21 @@ def test_readme_kat(gpu):
     (16, 8, 0.0, 512, 11), (32, 16, 0.0, 256, 12), (16, 8, 0.9, 64, 13), (32, 16, 0.9, 32, 14),
     (3, 5, 0.0, 128, 15), (7, 0, 0.0, 64, 16), (1, 1, 0.0, 64, 17), (10, 3, 0.5, 128, 18),
     (2, 31, 0.0, 64, 19), (30, 17, 0.0, 64, 20), (62, 1, 0.0, 32, 21), (5, 11, 0.3, 128, 22),
+    (32, 32, 0.0, 64, 23), (40, 24, 0.0, 32, 24), (12, 12, 0.0, 128, 25), (20, 28, 0.0, 64, 26),
 ])
-def test_random_qp_vs_oracle(gpu, oracle_lib, n, m, sp, B, seed):
+@pytest.mark.parametrize("ls", LS)
+def test_random_qp_vs_oracle(gpu, oracle_lib, n, m, sp, B, seed, ls):
+    if ls == "dense" and n + 2 * m > 64:
+        pytest.skip("dense LU covers n + 2m <= 64")
     theta = generate_random_parameter(np.random.default_rng(seed), n, m, sp, batch=B)
-    kw = dict(tol=1e-6)
+    kw = dict(tol=1e-6, linear_solver=ls)
     got = solve_batch(0, n, m, theta, trace_len=TRACE, **kw)
     ref = oracle_lib.solve_batch(0, n, m, theta, trace_len=TRACE, **kw)
     assert_parity(got, ref)
 
 
-def test_affine_family_vs_oracle(gpu, oracle_lib):
+@pytest.mark.parametrize("ls", LS)
+def test_affine_family_vs_oracle(gpu, oracle_lib, ls):
     rng = np.random.default_rng(5)
     for n, m in [(8, 4), (16, 8), (20, 22), (4, 30)]:
         B = 64
@@ -107,8 +115,8 @@ def test_affine_family_vs_oracle(gpu, oracle_lib):
             Sm = rng.standard_normal((m, m)) * 0.1; S = Sm @ Sm.T
             g = rng.standard_normal(n); h = rng.standard_normal(m)
             theta[b] = np.concatenate([P.flatten("F"), Q.flatten("F"), R.flatten("F"), S.flatten("F"), g, h])
-        got = solve_batch(1, n, m, theta, trace_len=TRACE, tol=1e-6)
-        ref = oracle_lib.solve_batch(1, n, m, theta, trace_len=TRACE, tol=1e-6)
+        got = solve_batch(1, n, m, theta, trace_len=TRACE, tol=1e-6, linear_solver=ls)
+        ref = oracle_lib.solve_batch(1, n, m, theta, trace_len=TRACE, tol=1e-6, linear_solver=ls)
         assert_parity(got, ref)
 
 
@@ -117,25 +125,29 @@ def test_affine_family_vs_oracle(gpu, oracle_lib):
     dict(max_inner_iters=3), dict(max_outer_iters=2), dict(min_stepsize=1e-2), dict(decay=0.3, tau=0.9),
     dict(tightening_rate=0.3, loosening_rate=0.2), dict(min_stepsize=1e-12),
 ])
-def test_params_vs_oracle(gpu, oracle_lib, kw):
+@pytest.mark.parametrize("ls", LS)
+def test_params_vs_oracle(gpu, oracle_lib, kw, ls):
+    kw = dict(kw, linear_solver=ls)
     theta = generate_random_parameter(np.random.default_rng(7), 16, 8, 0.2, batch=128)
     got = solve_batch(0, 16, 8, theta, trace_len=TRACE, **kw)
     ref = oracle_lib.solve_batch(0, 16, 8, theta, trace_len=TRACE, **kw)
     assert_parity(got, ref)
 
 
-def test_warm_start_vs_oracle(gpu, oracle_lib):
+@pytest.mark.parametrize("ls", LS)
+def test_warm_start_vs_oracle(gpu, oracle_lib, ls):
     """Warm starts (README.md:69-80; src/solver.jl:39-41)."""
     rng = np.random.default_rng(8)
     n, m, B = 32, 16, 64
     theta = generate_random_parameter(rng, n, m, 0.0, batch=B)
     x0 = rng.standard_normal((B, n)); y0 = rng.random((B, m)) + 0.1; s0 = rng.random((B, m)) + 0.1
-    got = solve_batch(0, n, m, theta, x0=x0, y0=y0, s0=s0, trace_len=TRACE, tol=1e-6)
-    ref = oracle_lib.solve_batch(0, n, m, theta, x0=x0, y0=y0, s0=s0, trace_len=TRACE, tol=1e-6)
+    got = solve_batch(0, n, m, theta, x0=x0, y0=y0, s0=s0, trace_len=TRACE, tol=1e-6, linear_solver=ls)
+    ref = oracle_lib.solve_batch(0, n, m, theta, x0=x0, y0=y0, s0=s0, trace_len=TRACE, tol=1e-6, linear_solver=ls)
     assert_parity(got, ref)
 
 
-def test_edge_inputs(gpu, oracle_lib):
+@pytest.mark.parametrize("ls", LS)
+def test_edge_inputs(gpu, oracle_lib, ls):
     """Singular Jacobians, NaN/Inf parameters, zero-size batch."""
     n, m = 4, 4
     p = _abi.theta_dim(0, n, m)
@@ -145,11 +157,23 @@ def test_edge_inputs(gpu, oracle_lib):
     th[3, -1] = np.inf              # Inf in ϕ
     th[4, n * n:n * n + m * n] = 0  # A = 0 → constraints inactive
     th[5, :] *= 1e150               # overflow-scale data
-    got = solve_batch(0, n, m, th, trace_len=TRACE)
-    ref = oracle_lib.solve_batch(0, n, m, th, trace_len=TRACE)
+    got = solve_batch(0, n, m, th, trace_len=TRACE, linear_solver=ls)
+    ref = oracle_lib.solve_batch(0, n, m, th, trace_len=TRACE, linear_solver=ls)
     assert_parity(got, ref)
-    empty = solve_batch(0, n, m, np.empty((0, p)))
+    empty = solve_batch(0, n, m, np.empty((0, p)), linear_solver=ls)
     assert empty["x"].shape == (0, n)
+
+
+def test_unsupported_sizes(gpu):
+    """Sizes outside the register-resident kernels are an error (MCPXError), not a silent fallback."""
+    from mcp_amd import MCPXError
+
+    th = generate_random_parameter(np.random.default_rng(0), 32, 32, 0.0, batch=2)
+    with pytest.raises(MCPXError):
+        solve_batch(0, 32, 32, th, linear_solver="dense")  # n + 2m = 96
+    th = generate_random_parameter(np.random.default_rng(0), 40, 30, 0.0, batch=2)
+    with pytest.raises(MCPXError):
+        solve_batch(0, 40, 30, th)  # n + m = 70
 
 
 def test_device_api_matches_host_api(gpu):
@@ -166,7 +190,8 @@ def test_device_api_matches_host_api(gpu):
         np.testing.assert_array_equal(dev[k].cpu().numpy(), host[k], err_msg=k)
 
 
-def test_full_size_properties(gpu, oracle_lib):
+@pytest.mark.parametrize("ls", LS)
+def test_full_size_properties(gpu, oracle_lib, ls):
     """BASELINE C3 at full size (B=65536, N=64) on the GPU: a random sample is
     checked bit-for-bit against the oracle, and size-independent properties hold
     for every instance (iterate feasibility s,y ≥ 0 when solved, the active set
@@ -179,7 +204,7 @@ def test_full_size_properties(gpu, oracle_lib):
     n, m, B = 32, 16, 65536
     g = torch.Generator(device="cuda").manual_seed(1234)
     theta = generate_random_parameter_torch(g, n, m, B)
-    out = solve_batch_device(0, n, m, theta, tol=1e-6)
+    out = solve_batch_device(0, n, m, theta, tol=1e-6, linear_solver=ls)
     torch.cuda.synchronize()
     r = {k: v.cpu().numpy() for k, v in out.items() if v is not None}
     solved = r["status"] == 0
@@ -190,7 +215,7 @@ def test_full_size_properties(gpu, oracle_lib):
     np.testing.assert_array_equal(bits, r["y"] > r["s"])
     idx = np.random.default_rng(0).choice(B, 96, replace=False)
     th = theta[idx].cpu().numpy()
-    ref = oracle_lib.solve_batch(0, n, m, th, tol=1e-6, nthreads=8)
+    ref = oracle_lib.solve_batch(0, n, m, th, tol=1e-6, nthreads=8, linear_solver=ls)
     sub = {k: v[idx] for k, v in r.items()}
     sub["active_mask"] = sub["active_mask"].astype(np.uint64).reshape(-1, 1)
     sub["alpha_trace"] = np.zeros((len(idx), 0, 2), np.uint8)

@@ -2,7 +2,8 @@
 // Not a timing build — read the shares, not the absolute time.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -DMCPX_STAMPS=1 \
 //          tools/phase_profile.hip mcp_amd/csrc/mcpx_api.cpp -o tools/phase_profile
-#include "../mcp_amd/csrc/ipm_kernel.hip"
+// Run:   tools/phase_profile n m B {spec|gen|gen64|dense}
+#include "../mcp_amd/csrc/ipm_kernel_impl.hpp"
 
 #include <cstdio>
 #include <cstring>
@@ -32,7 +33,8 @@ int main(int argc, char** argv) {
   }
   mcpx_desc d{0, n, m, 0, B, p};
   mcpx_params prm;
-  mcpx_default_params(&prm);
+  prm.max_inner_iters = 20;
+  prm.max_outer_iters = 50;
   prm.tol = 1e-6;
   double *dth, *x, *y, *s, *kkt, *eps;
   int *outer, *status, *newton;
@@ -44,7 +46,6 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&outer, B * 4); (void)hipMalloc(&status, B * 4); (void)hipMalloc(&newton, B * 4);
   (void)hipMalloc(&stamps, (size_t)B * 4 * 8);
   mcpx::KernelArgs a;
-  int nmax = 0;
   // reuse the ABI's parameter preparation through a normal call first (fills nothing here)
   std::memset((void*)&a, 0, sizeof a);
   a.theta = dth; a.theta_ld = p; a.x = x; a.y = y; a.s = s; a.kkt_error = kkt; a.eps = eps;
@@ -52,10 +53,17 @@ int main(int argc, char** argv) {
   a.n = n; a.m = m; a.max_inner = prm.max_inner_iters; a.max_outer = prm.max_outer_iters; a.tol = prm.tol;
   a.decay = 0.5; a.c_tau = 1.0 - 0.995; a.n_trials = 15;
   for (int k = 0; k <= prm.max_inner_iters; ++k) { a.tight[k] = 1 - exp(-0.1 * k); a.loose[k] = 1 + exp(-0.5 * k); }
-  const int N = n + 2 * m;
-  nmax = N <= 8 ? 8 : N <= 16 ? 16 : N <= 32 ? 32 : 64;
+  const char* mode = argc > 4 ? argv[4] : "spec";
+  a.family = 0;
+  a.reduced = strcmp(mode, "dense") != 0;
   for (int rep = 0; rep < 2; ++rep) {
-    (void)mcpx::launch_ipm(nmax, 0, a, B, 0, getenv("MCPX_GENERIC_KERNELS") == nullptr);
+    hipError_t e = hipErrorInvalidValue;
+    if (!strcmp(mode, "spec") && n == 32 && m == 16) e = mcpx::launch_one<48, 0, 32, 16, true>(a, B, 0);
+    else if (!strcmp(mode, "spec") && n == 16 && m == 8) e = mcpx::launch_one<24, 0, 16, 8, true>(a, B, 0);
+    else if (!strcmp(mode, "gen") && n + m <= 48) e = mcpx::launch_one<48, 0, 0, 0, true>(a, B, 0);
+    else if (!strcmp(mode, "gen64")) e = mcpx::launch_one<64, 0, 0, 0, true>(a, B, 0);
+    else if (!strcmp(mode, "dense")) e = mcpx::launch_one<64, 0, 0, 0, false>(a, B, 0);
+    if (e != hipSuccess) { printf("launch failed / unsupported mode: %s\n", hipGetErrorString(e)); return 1; }
     (void)hipDeviceSynchronize();
   }
   std::vector<uint64_t> st((size_t)B * 4);
@@ -66,7 +74,7 @@ int main(int argc, char** argv) {
   for (int b = 0; b < B; ++b) { for (int i = 0; i < 4; ++i) tot[i] += st[(size_t)b * 4 + i]; nsteps += nw[b]; }
   const double all = tot[0] + tot[1] + tot[2] + tot[3];
   const char* nm[] = {"assemble+kkt", "LU+fwd", "backsub", "linesearch+update"};
-  printf("n=%d m=%d B=%d  mean newton %.2f  wave-cycles per Newton step %.0f\n", n, m, B, nsteps / B, all / nsteps);
+  printf("[%s] n=%d m=%d B=%d  mean newton %.2f  wave-cycles per Newton step %.0f\n", mode, n, m, B, nsteps / B, all / nsteps);
   for (int i = 0; i < 4; ++i) printf("  %-18s %5.1f%%  %8.0f cyc/step\n", nm[i], 100 * tot[i] / all, tot[i] / nsteps);
   return 0;
 }
