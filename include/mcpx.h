@@ -79,9 +79,15 @@ extern "C" {
  *                         then dense LU with partial pivoting of the (n+m)-dim
  *                         Schur complement (default; N ≤ 64 means n + m ≤ 64);
  *  MCPX_LINSOLVE_DENSE    dense LU with partial pivoting of the full
- *                         (n+2m)-dim system (n + 2m ≤ 64). */
+ *                         (n+2m)-dim system (n + 2m ≤ 64);
+ *  MCPX_LINSOLVE_SCHUR    QP family only (∂H/∂y = 0): after the slack block,
+ *                         the now-diagonal y block is eliminated as well and
+ *                         the n×n Schur complement (M + tol·I) + Aᵀ D⁻¹ A is
+ *                         formed on the matrix cores (fp64 MFMA) and solved by
+ *                         dense LU with partial pivoting (n + m ≤ 64). */
 #define MCPX_LINSOLVE_REDUCED 0
 #define MCPX_LINSOLVE_DENSE 1
+#define MCPX_LINSOLVE_SCHUR 2
 
 /* Solver keyword arguments, same names and defaults as src/solver.jl:42-50;
  * tau and decay are the hard-coded defaults of

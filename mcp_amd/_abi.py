@@ -18,7 +18,8 @@ MAX_KKT_DIM = 64
 
 LINSOLVE_REDUCED = 0
 LINSOLVE_DENSE = 1
-LINEAR_SOLVERS = {"reduced": LINSOLVE_REDUCED, "dense": LINSOLVE_DENSE}
+LINSOLVE_SCHUR = 2
+LINEAR_SOLVERS = {"reduced": LINSOLVE_REDUCED, "dense": LINSOLVE_DENSE, "schur": LINSOLVE_SCHUR}
 MAX_INNER_ITERS = 128
 MAX_LS_TRIALS = 64
 

@@ -20,14 +20,16 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libmcpx.so")
 SOURCES = [os.path.join(CSRC, f) for f in (
-    "ipm_inst_red_qp.hip", "ipm_inst_spec.hip", "ipm_inst_red_aff.hip", "ipm_inst_dense_qp.hip",
-    "ipm_inst_dense_aff.hip", "mcpx_api.cpp")]
+    "ipm_inst_red_qp.hip", "ipm_inst_spec.hip", "ipm_inst_schur_qp.hip", "ipm_inst_red_aff.hip",
+    "ipm_inst_dense_qp.hip", "ipm_inst_dense_aff.hip", "mcpx_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("ipm_kernel.h", "ipm_kernel_impl.hpp", "bcast_group.inc")] + [
     os.path.join(ROOT, "include", "mcpx.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
+# -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (dead during the LU)
+# instead of AGPRs, which would add to every wave's register allocation.
 FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-fPIC",
-         "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
+         "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
 
 
 def _stale() -> bool:

@@ -29,7 +29,7 @@ struct KernelArgs {
   int32_t trace_len;
   int32_t n, m;
   int32_t family;   // MCPX_FAMILY_*
-  int32_t reduced;  // 1: MCPX_LINSOLVE_REDUCED, 0: MCPX_LINSOLVE_DENSE
+  int32_t solver;   // MCPX_LINSOLVE_*
   int32_t max_inner, max_outer;
   int32_t n_trials;  // line-search trials e = 0 .. n_trials-1 (α_e = decayᵉ)
   double tol;
@@ -41,10 +41,11 @@ struct KernelArgs {
 
 // Launchers of the register-resident solver: one 64-lane wave (= one
 // workgroup) per instance.  nmax ∈ {8,16,24,32,48,64} ≥ the linear-system dimension
-// (n + m reduced, n + 2m dense).  Each returns hipErrorNotFound /
+// (n + m reduced, n + 2m dense, n Schur).  Each returns hipErrorNotFound /
 // hipErrorInvalidValue when it has no matching kernel.
-hipError_t launch_ipm_spec(int family, bool reduced, int n, int m, const KernelArgs& a, int64_t batch,
+hipError_t launch_ipm_spec(int family, int solver, int n, int m, const KernelArgs& a, int64_t batch,
                            hipStream_t st);
+hipError_t launch_ipm_schur_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 hipError_t launch_ipm_red_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 hipError_t launch_ipm_red_aff(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 hipError_t launch_ipm_dense_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);

@@ -315,13 +315,143 @@ __device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int
   return true;
 }
 
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// acc ← fma chain over j < cnt of (±p[j·st]) · q[j], q in LDS.  The global
+// loads are issued BATCH at a time from clamped (always valid) addresses and
+// consumed afterwards, so a batch pays one memory latency instead of BATCH
+// (a plain loop compiles to load → s_waitcnt vmcnt(0) → fma per element).
+template <int BATCH, bool NEG>
+__device__ __forceinline__ double dot_strided(const double* __restrict__ p, int st, const double* q, int cnt,
+                                              double acc) {
+  for (int j0 = 0; j0 < cnt; j0 += BATCH) {
+    double t[BATCH];
+#pragma unroll
+    for (int b = 0; b < BATCH; ++b) t[b] = p[min(j0 + b, cnt - 1) * st];
+#pragma unroll
+    for (int b = 0; b < BATCH; ++b)
+      if (j0 + b < cnt) acc = fma(NEG ? -t[b] : t[b], q[j0 + b], acc);
+    __builtin_amdgcn_sched_barrier(0);  // at most BATCH loads in flight (register budget)
+  }
+  return acc;
+}
+
+// SCHUR path (QP family), part 1: residuals.  x-lanes compute F_G, y-lanes
+// (which also own s_k) F_H and F_C; same fma order as family_row() of the
+// oracle.
+template <int BATCH>
+__device__ __forceinline__ void qp_residuals(const double* __restrict__ th, const double* zs, int ln, int n,
+                                             int m, double eps, double s_own, double& F, double& Fc) {
+  const bool rg = ln < n, rh = ln >= n && ln < n + m;
+  const int kh = ln - n, nn = n * n, nm = n * m;
+  const double* px = rg ? th + ln : (rh ? th + nn + kh : th);
+  const int sx = rg ? n : (rh ? m : 0);
+  double acc = dot_strided<BATCH, false>(px, sx, zs, n, 0.0);  // M_ij x_j  |  A_kj x_j
+  const double acc_y = dot_strided<BATCH, true>(th + nn + (rg ? ln * m : 0), 1, zs + n, m, acc);  // − A_ki y_k
+  if (rg) acc = acc_y;
+  F = 0.0;
+  Fc = 0.0;
+  if (rg) F = acc - th[nn + nm + m + ln];                       // G = Mx − Aᵀy − ϕ
+  if (rh) {
+    F = (acc - th[nn + nm + kh]) - s_own;                       // H − s
+    Fc = s_own * zs[n + kh] - eps;                              // s⊙y − ϵ
+  }
+}
+
+// SCHUR path, part 2: the n×n Schur complement S = (M + tol·I) + Aᵀ D⁻¹ A on the
+// fp64 matrix cores.  v_mfma_f64_16x16x4_f64 is an ordered fma chain over its
+// 4 k's (tools/ubench_mfma64.hip), so K-chunked accumulation reproduces the
+// oracle's sequential fma chain bit for bit (k ≥ m are zero operands).
+// Operands come straight from θ in fragment layout: A-fragment lane l holds
+// A_ki with i = 16I + (l & 15), k = 4c + (l >> 4) (contiguous in k); the
+// B-fragment holds A_kj / D_k with j = 16J + (l & 15).  The tiles land in LDS
+// (row-major, stride NMAX+1) and each x-lane reads back its row.
+template <int NMAX>
+__device__ __forceinline__ void qp_schur_rows(const double* __restrict__ th, const double* sD, double* sS, int ln,
+                                              int n, int m, double tol, double (&a)[NMAX]) {
+  constexpr int NT = (NMAX + 15) / 16;
+  const int nn = n * n;
+  const int lr = ln >> 4, lc = ln & 15;
+  d4 acc[NT][NT];
+  {  // C = M + tol·I, all NT·NT·4 loads issued before any use
+    double mv[NT][NT][4];
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = 0; J < NT; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = min(16 * I + lr + 4 * r, n - 1), col = min(16 * J + lc, n - 1);
+          mv[I][J][r] = th[col * n + row];
+        }
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = 0; J < NT; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * I + lr + 4 * r, col = 16 * J + lc;
+          const bool in = row < n && col < n;
+          const double v = mv[I][J][r];
+          acc[I][J][r] = in ? (row == col ? v + tol : v) : 0.0;  // M_ij (+ tol on the diagonal)
+        }
+  }
+  const int kc = (m + 3) / 4;
+  // K-chunk c: lane l's A_ki for i = 16I + lc, k = 4c + lr; loads of chunk c+1
+  // are issued before the MFMAs of chunk c (software pipelining)
+  double nxt[NT];
+#pragma unroll
+  for (int I = 0; I < NT; ++I) nxt[I] = th[nn + min(16 * I + lc, n - 1) * m + min(lr, max(m - 1, 0))];
+  for (int c = 0; c < kc; ++c) {
+    const int k = 4 * c + lr;
+    const bool kin = k < m;
+    const double dk = sD[kin ? k : 0];
+    double cur[NT];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) cur[I] = nxt[I];
+    if (c + 1 < kc) {
+      const int k1 = min(k + 4, m - 1);
+#pragma unroll
+      for (int I = 0; I < NT; ++I) nxt[I] = th[nn + min(16 * I + lc, n - 1) * m + k1];
+    }
+    double af[NT], bf[NT];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+      const bool in = kin && 16 * I + lc < n;
+      af[I] = in ? cur[I] : 0.0;        // A_ki
+      bf[I] = in ? cur[I] / dk : 0.0;   // A_kj / D_k  (j = 16J + lc: the same index pattern)
+    }
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = 0; J < NT; ++J) acc[I][J] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[I], bf[J], acc[I][J], 0, 0, 0);
+  }
+#pragma unroll
+  for (int I = 0; I < NT; ++I)
+#pragma unroll
+    for (int J = 0; J < NT; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * I + lr + 4 * r, col = 16 * J + lc;
+        if (row < n && col < n) sS[row * (NMAX + 1) + col] = acc[I][J][r];
+      }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) a[j] = (ln < n && j < n) ? sS[min(ln, NMAX - 1) * (NMAX + 1) + j] : 0.0;
+}
+
 }  // namespace
 
 // NC, MC > 0: compile-time (n, m) specialisation; 0: runtime n, m.
-// RED: slack-eliminated (n+m)-dim system; otherwise the full (n+2m)-dim one.
-template <int NMAX, int FAMILY, int NC, int MC, bool RED>
+// SOLVER: MCPX_LINSOLVE_REDUCED (slack-eliminated (n+m)-dim system), _DENSE
+// (full (n+2m)-dim system) or _SCHUR (QP family, n×n Schur complement on MFMA).
+template <int NMAX, int FAMILY, int NC, int MC, int SOLVER>
 __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
+  constexpr bool RED = SOLVER != MCPX_LINSOLVE_DENSE;  // lanes [0,n) x, [n,n+m) (y, s)
+  constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR;
   __shared__ double zs[64];
+  __shared__ double sD[SCH ? 64 : 1], sT[SCH ? 64 : 1];
+  __shared__ double sS[SCH ? NMAX * (NMAX + 1) : 1];
   const int lane = threadIdx.x;
   const int64_t inst = blockIdx.x;
   const int n0 = NC ? NC : args.n, m0 = MC ? MC : args.m;
@@ -356,7 +486,7 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
     status = 0;      // :73
     while (kkt > eps && inner < args.max_inner) {  // :75
       const int n = NC ? NC : opaque(n0), m = MC ? MC : opaque(m0);
-      const int NS = RED ? n + m : n + 2 * m;             // rows of the linear system
+      const int NS = SCH ? n : (RED ? n + m : n + 2 * m);  // rows of the linear system
       const double* __restrict__ th = th0 + opaque64(0);  // stays a global pointer
       const int ln = opaque_lane(lane);
       // ---- F!, ∇F_z! (:79-81) --------------------------------------------
@@ -364,23 +494,51 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       zs[ln] = z;
       __syncthreads();
       double a[NMAX];
-      double F, Fc, rhs, w;
-      assemble_row<NMAX, FAMILY, RED, (NC > 0)>(th, zs, ln, n, m, eps, tol, s, a, F, Fc, rhs, w);
-      // ‖F‖∞ with NaN propagation (:107), taken now, committed after the step
+      double F, Fc, rhs, w = 1.0;
       const bool rh = ln >= n && ln < n + m;
-      double aF = (ln < NS) ? fabs(F) : 0.0;
+      double D = 1.0, ryr = 0.0;  // SCHUR: y-block pivot and reduced y right-hand side
+      if constexpr (SCH) {
+        qp_residuals<8>(th, zs, ln, n, m, eps, s, F, Fc);
+        rhs = -F;
+        if (rh) {  // eliminate δs_k (pivot w_k) and then δy_k (pivot D_k)
+          w = zs[ln] + tol;
+          D = tol + s / w;
+          ryr = (-F) - (Fc / w);
+          sD[ln - n] = D;
+          sT[ln - n] = ryr / D;
+        }
+      } else {
+        assemble_row<NMAX, FAMILY, RED, (NC > 0)>(th, zs, ln, n, m, eps, tol, s, a, F, Fc, rhs, w);
+      }
+      // ‖F‖∞ with NaN propagation (:107), taken now, committed after the step
+      double aF = (ln < (RED ? n + m : NS)) ? fabs(F) : 0.0;
       if (RED && rh) aF = max_nan(aF, fabs(Fc));
       const bool any_nan = ballot(aF != aF) != 0ull;
       const double kkt_step = any_nan ? __builtin_nan("") : wave_max_nonneg(aF);
+      if constexpr (SCH) {
+        __syncthreads();
+        qp_schur_rows<NMAX>(th, sD, sS, ln, n, m, tol, a);
+        // rr_i = −F_Gi + Σ_k A_ki ty_k  (x-lanes; other lanes' value unused)
+        rhs = dot_strided<8, false>(th + n * n + (ln < n ? ln : 0) * m, 1, sT, m, rhs);
+      }
       MCPX_STAMP(0);
 
       // ---- dense LU with partial pivoting (:81-83) -----------------------
       double dz = 0.0;
-      const bool ok = lu_solve_rows<NMAX>(a, rhs, NS, ln, dz);
+      // the LU gets an opaque dimension even in the compile-time kernels: with a
+      // constant N the allocator keeps ~40 more VGPRs live (fewer waves/SIMD)
+      const bool ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
       MCPX_STAMP(1);
       if (!ok) {
         status = 1;
         break;
+      }
+      if constexpr (SCH) {  // δy_k = (ry_k − Σ_j A_kj δx_j) / D_k
+        __syncthreads();
+        zs[ln] = dz;
+        __syncthreads();
+        const double acc = dot_strided<8, true>(th + n * n + (rh ? ln - n : 0), m, zs, n, ryr);
+        if (rh) dz = acc / D;
       }
       double ds = 0.0;
       if (RED && rh) ds = fma(-s, dz, -Fc) / w;  // δs_k = (−F_Ck − s_k δy_k) / w_k
@@ -472,9 +630,9 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
 }
 
 // Launch helper used by the instantiation units.
-template <int NMAX, int FAMILY, int NC, int MC, bool RED>
+template <int NMAX, int FAMILY, int NC, int MC, int SOLVER>
 hipError_t launch_one(const KernelArgs& args, int64_t batch, hipStream_t stream) {
-  hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, RED>), dim3((unsigned)batch), dim3(64), 0, stream,
+  hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER>), dim3((unsigned)batch), dim3(64), 0, stream,
                      args);
   return hipGetLastError();
 }

@@ -72,14 +72,18 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   if (d->n + d->m < 1) return fail(MCPX_EINVAL, "empty problem (n = m = 0)");
   if (d->batch < 0) return fail(MCPX_EINVAL, "negative batch");
   if (d->theta_ld < pd) return fail(MCPX_EINVAL, "theta_ld %lld < parameter dimension %lld", (long long)d->theta_ld, (long long)pd);
-  if (p->linear_solver != MCPX_LINSOLVE_REDUCED && p->linear_solver != MCPX_LINSOLVE_DENSE)
-    return fail(MCPX_EINVAL, "unknown linear_solver %d", p->linear_solver);
-  const bool red = p->linear_solver == MCPX_LINSOLVE_REDUCED;
-  const int N = red ? d->n + d->m : d->n + 2 * d->m;
+  const int ls = p->linear_solver;
+  if (ls != MCPX_LINSOLVE_REDUCED && ls != MCPX_LINSOLVE_DENSE && ls != MCPX_LINSOLVE_SCHUR)
+    return fail(MCPX_EINVAL, "unknown linear_solver %d", ls);
+  if (ls == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP)
+    return fail(MCPX_EINVAL, "linear_solver=schur needs the QP family (dH/dy = 0)");
+  const int N = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : (ls == MCPX_LINSOLVE_REDUCED ? d->n + d->m : d->n);
+  const int lanes = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : d->n + d->m;  // one wave: one lane per row
   *nmax = pick_nmax(N);
-  if (*nmax < 0)
-    return fail(MCPX_EUNSUPPORTED, "linear-system dimension %d (%s) > %d not supported by the register-resident kernel",
-                N, red ? "n+m" : "n+2m", MCPX_MAX_KKT_DIM);
+  if (*nmax < 0 || lanes > MCPX_MAX_KKT_DIM)
+    return fail(MCPX_EUNSUPPORTED, "problem size n=%d m=%d exceeds the register-resident kernel for this "
+                "linear_solver (reduced/schur: n+m <= %d, dense: n+2m <= %d)", d->n, d->m, MCPX_MAX_KKT_DIM,
+                MCPX_MAX_KKT_DIM);
   if (!(p->tol > 0) || !(p->min_stepsize > 0) || !(p->decay > 0 && p->decay < 1) || std::isnan(p->tau) ||
       std::isnan(p->tightening_rate) || std::isnan(p->loosening_rate) || p->max_inner_iters < 1 ||
       p->max_outer_iters < 1)
@@ -89,7 +93,7 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   std::memset(a, 0, sizeof *a);
   a->n = d->n;
   a->m = d->m;
-  a->reduced = red ? 1 : 0;
+  a->solver = ls;
   a->family = d->family;
   a->theta_ld = d->theta_ld;
   a->max_inner = p->max_inner_iters;
@@ -118,13 +122,18 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
 // MCPX_GENERIC_KERNELS is not set), else the runtime-(n, m) kernel for nmax.
 hipError_t launch(int nmax, const mcpx::KernelArgs& a, int64_t nb, hipStream_t st) {
   if (specialized_enabled()) {
-    const hipError_t e = mcpx::launch_ipm_spec(a.family, a.reduced != 0, a.n, a.m, a, nb, st);
+    const hipError_t e = mcpx::launch_ipm_spec(a.family, a.solver, a.n, a.m, a, nb, st);
     if (e != hipErrorNotFound) return e;
   }
-  if (a.reduced) return a.family == MCPX_FAMILY_QP ? mcpx::launch_ipm_red_qp(nmax, a, nb, st)
-                                                   : mcpx::launch_ipm_red_aff(nmax, a, nb, st);
-  return a.family == MCPX_FAMILY_QP ? mcpx::launch_ipm_dense_qp(nmax, a, nb, st)
-                                    : mcpx::launch_ipm_dense_aff(nmax, a, nb, st);
+  const bool qp = a.family == MCPX_FAMILY_QP;
+  switch (a.solver) {
+    case MCPX_LINSOLVE_REDUCED:
+      return qp ? mcpx::launch_ipm_red_qp(nmax, a, nb, st) : mcpx::launch_ipm_red_aff(nmax, a, nb, st);
+    case MCPX_LINSOLVE_DENSE:
+      return qp ? mcpx::launch_ipm_dense_qp(nmax, a, nb, st) : mcpx::launch_ipm_dense_aff(nmax, a, nb, st);
+    default:
+      return mcpx::launch_ipm_schur_qp(nmax, a, nb, st);
+  }
 }
 
 int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,

@@ -33,6 +33,13 @@
  *    d_k = s_k / w_k added to the (H_k, y_k) diagonal entry after its tol,
  *    rhs_Hk = (−F_Hk) − (F_Ck / w_k); the (n+m) system is solved by the LU
  *    above and δs_k = fma(−s_k, δy_k, −F_Ck) / w_k;
+ *  - linear_solver = MCPX_LINSOLVE_SCHUR (QP family) also eliminates the
+ *    diagonal y block D_k = (0 + tol) + d_k: ry_k = (−F_Hk) − (F_Ck / w_k),
+ *    ty_k = ry_k / D_k; S_ij = fma chain over k = 0 .. 4⌈m/4⌉−1 starting at
+ *    (M_ij + tol·[i=j]) of A_ki · (A_kj / D_k) (k ≥ m contributes fma(0, 0, ·),
+ *    the zero padding of the fp64 MFMA K-chunks); rr_i = fma chain over k of
+ *    A_ki · ty_k starting at −F_Gi; δx = LU(S) \ rr; δy_k = (fma chain over j
+ *    of −A_kj · δx_j starting at ry_k) / D_k; δs as above;
  *    (UMFPACK itself, LinearSolve 2.38 UMFPACKFactorization, is a third-party
  *    sparse LU not present here: this dense LU replaces it, results differ in
  *    rounding only);
@@ -65,7 +72,8 @@ int oracle_build_tables(const mcpx_params* p, oracle_tables* t) {
       !(p->tau == p->tau) || !(p->tightening_rate == p->tightening_rate) ||
       !(p->loosening_rate == p->loosening_rate) || p->max_inner_iters < 1 ||
       p->max_outer_iters < 1 ||
-      (p->linear_solver != MCPX_LINSOLVE_REDUCED && p->linear_solver != MCPX_LINSOLVE_DENSE))
+      (p->linear_solver != MCPX_LINSOLVE_REDUCED && p->linear_solver != MCPX_LINSOLVE_DENSE &&
+       p->linear_solver != MCPX_LINSOLVE_SCHUR))
     return MCPX_EINVAL;
   if (p->max_inner_iters > MCPX_MAX_INNER_ITERS) return MCPX_EUNSUPPORTED;
   /* src/solver.jl:128-135: α = 1; while violated: if α < tol → NaN; α *= decay */
@@ -217,7 +225,7 @@ static int linesearch_exponent(const double* v, const double* d, int cnt, const 
 }
 
 typedef struct ws {
-  double *J, *Jr, *row, *F, *b, *dz, *z;
+  double *J, *Jr, *row, *F, *b, *dz, *z, *sD, *sry, *sty;
   int *remaining, *step_of, *prow;
 } ws;
 
@@ -225,6 +233,9 @@ static int ws_alloc(ws* w, int N) {
   w->J = (double*)malloc(sizeof(double) * (size_t)N * N);
   w->Jr = (double*)malloc(sizeof(double) * (size_t)N * N);
   w->row = (double*)malloc(sizeof(double) * N);
+  w->sD = (double*)malloc(sizeof(double) * N);
+  w->sry = (double*)malloc(sizeof(double) * N);
+  w->sty = (double*)malloc(sizeof(double) * N);
   w->F = (double*)malloc(sizeof(double) * N);
   w->b = (double*)malloc(sizeof(double) * N);
   w->dz = (double*)malloc(sizeof(double) * N);
@@ -232,10 +243,10 @@ static int ws_alloc(ws* w, int N) {
   w->remaining = (int*)malloc(sizeof(int) * N);
   w->step_of = (int*)malloc(sizeof(int) * N);
   w->prow = (int*)malloc(sizeof(int) * N);
-  return (w->J && w->Jr && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
+  return (w->J && w->Jr && w->sD && w->sry && w->sty && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
 }
 static void ws_free(ws* w) {
-  free(w->J); free(w->Jr); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
+  free(w->J); free(w->Jr); free(w->sD); free(w->sry); free(w->sty); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
   free(w->remaining); free(w->step_of); free(w->prow);
 }
 
@@ -269,6 +280,51 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
         if (lu_solve(N, w->J, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
           status = MCPX_STATUS_FAILED;
           break;
+        }
+      } else if (p->linear_solver == MCPX_LINSOLVE_SCHUR) {
+        /* slack block, then the diagonal y block: n×n Schur complement (QP family) */
+        const int m4 = (m + 3) / 4 * 4;
+        for (int k = 0; k < m; ++k) {
+          const int h = n + k, c = n + m + k;
+          const double wk = w->J[(size_t)c * N + c];  /* y_k + tol */
+          const double D = w->J[(size_t)h * N + h] + z[c] / wk;
+          const double ry = w->b[h] - (w->F[c] / wk);
+          w->sD[k] = D;
+          w->sry[k] = ry;
+          w->sty[k] = ry / D;
+        }
+        for (int i = 0; i < n; ++i)
+          for (int j = 0; j < n; ++j) {
+            double acc = w->J[(size_t)i * N + j]; /* M_ij (+ tol) */
+            for (int k = 0; k < m4; ++k) {
+              if (k < m) {
+                const double aki = -w->J[(size_t)i * N + n + k]; /* A_ki */
+                const double akj = w->J[(size_t)(n + k) * N + j];  /* A_kj */
+                acc = fma(aki, akj / w->sD[k], acc);
+              } else {
+                acc = fma(0.0, 0.0, acc);
+              }
+            }
+            w->Jr[(size_t)i * n + j] = acc;
+          }
+        for (int i = 0; i < n; ++i) {
+          double acc = w->b[i]; /* −F_Gi */
+          for (int k = 0; k < m; ++k) acc = fma(-w->J[(size_t)i * N + n + k], w->sty[k], acc);
+          w->b[i] = acc;
+        }
+        if (lu_solve(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
+          status = MCPX_STATUS_FAILED;
+          break;
+        }
+        for (int k = 0; k < m; ++k) {
+          double acc = w->sry[k];
+          for (int j = 0; j < n; ++j) acc = fma(-w->J[(size_t)(n + k) * N + j], w->dz[j], acc);
+          w->dz[n + k] = acc / w->sD[k];
+        }
+        for (int k = 0; k < m; ++k) {
+          const int c = n + m + k;
+          const double wk = w->J[(size_t)c * N + c];
+          w->dz[c] = fma(-z[c], w->dz[n + k], -w->F[c]) / wk;
         }
       } else {
         /* exact elimination of the slack block, then LU of the (n+m) Schur complement */
@@ -390,6 +446,7 @@ int oracle_solve_batch(const mcpx_desc* d, const double* theta, const double* x0
     return MCPX_EINVAL;
   const int64_t pd = oracle_theta_dim(d->family, d->n, d->m);
   if (pd < 0 || d->n + d->m < 1 || d->batch < 0 || d->theta_ld < pd) return MCPX_EINVAL;
+  if (p->linear_solver == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP) return MCPX_EINVAL;
   oracle_tables t;
   const int rc = oracle_build_tables(p, &t);
   if (rc) return rc;

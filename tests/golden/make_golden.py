@@ -99,6 +99,14 @@ def main():
     case("qp_n16_m8_sparse_dense_lu", 0, 16, 8,
          generate_random_parameter(np.random.default_rng(3), 16, 8, 0.9, batch=8), tol=1e-6, linear_solver="dense")
     case("game_clamp_dense", 1, 4, 8, game_clamp_theta([-1.0, 0.0, 1.0, 1.0]), tol=1e-4, linear_solver="dense")
+    # the MFMA Schur-complement solve (QP family)
+    case("readme_qp_schur", 0, 2, 2, readme_qp_theta([-0.5, 0.5]), linear_solver="schur")
+    case("qp_n16_m8_schur", 0, 16, 8, generate_random_parameter(np.random.default_rng(1), 16, 8, 0.0, batch=16),
+         tol=1e-6, linear_solver="schur")
+    case("qp_n32_m16_schur", 0, 32, 16, generate_random_parameter(np.random.default_rng(2), 32, 16, 0.0, batch=8),
+         tol=1e-6, linear_solver="schur")
+    case("qp_n16_m8_sparse_schur", 0, 16, 8,
+         generate_random_parameter(np.random.default_rng(3), 16, 8, 0.9, batch=8), tol=1e-6, linear_solver="schur")
 
 
 if __name__ == "__main__":

@@ -102,6 +102,11 @@ def test_size_limits():
                  _abi.make_params(linear_solver="dense")) == _abi.MCPX_EUNSUPPORTED
 
 
+def test_schur_needs_qp_family():
+    desc = _abi.Desc(1, 2, 2, 0, 1, _abi.theta_dim(1, 2, 2))
+    assert _call(desc, np.zeros(64), _abi.make_params(linear_solver="schur")) == _abi.MCPX_EINVAL
+
+
 def test_no_device_is_an_error_not_a_fallback():
     """Without a GPU the product path fails loudly (there is no CPU fallback)."""
     if lib().mcpx_device_count() > 0:

@@ -29,8 +29,9 @@ INT = ("outer_iters", "status", "newton_iters")
 
 def _rel(a, b):
     a, b = np.asarray(a, float), np.asarray(b, float)
-    both_nan = np.isnan(a) & np.isnan(b)
-    d = np.where(both_nan, 0.0, np.abs(a - b))
+    same = (a == b) | (np.isnan(a) & np.isnan(b))  # includes equal infinities
+    with np.errstate(invalid="ignore"):
+        d = np.where(same, 0.0, np.abs(a - b))
     scale = np.maximum(1.0, np.where(np.isfinite(b), np.abs(b), 1.0))
     return float(np.max(d / scale)) if d.size else 0.0
 
@@ -55,7 +56,7 @@ def _params_from(d):
     return kw
 
 
-LS = ["reduced", "dense"]
+LS = ["reduced", "dense", "schur"]
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(HERE, "golden", "*.npz"))),
@@ -95,6 +96,8 @@ def test_readme_kat(gpu):
 def test_random_qp_vs_oracle(gpu, oracle_lib, n, m, sp, B, seed, ls):
     if ls == "dense" and n + 2 * m > 64:
         pytest.skip("dense LU covers n + 2m <= 64")
+    if n + m > 64:
+        pytest.skip("one wave holds n + m <= 64 rows")
     theta = generate_random_parameter(np.random.default_rng(seed), n, m, sp, batch=B)
     kw = dict(tol=1e-6, linear_solver=ls)
     got = solve_batch(0, n, m, theta, trace_len=TRACE, **kw)
@@ -102,7 +105,7 @@ def test_random_qp_vs_oracle(gpu, oracle_lib, n, m, sp, B, seed, ls):
     assert_parity(got, ref)
 
 
-@pytest.mark.parametrize("ls", LS)
+@pytest.mark.parametrize("ls", ["reduced", "dense"])
 def test_affine_family_vs_oracle(gpu, oracle_lib, ls):
     rng = np.random.default_rng(5)
     for n, m in [(8, 4), (16, 8), (20, 22), (4, 30)]:
@@ -174,6 +177,12 @@ def test_unsupported_sizes(gpu):
     th = generate_random_parameter(np.random.default_rng(0), 40, 30, 0.0, batch=2)
     with pytest.raises(MCPXError):
         solve_batch(0, 40, 30, th)  # n + m = 70
+    with pytest.raises(MCPXError):
+        solve_batch(0, 40, 30, th, linear_solver="schur")
+    from mcp_amd import _abi as abi
+    tha = np.zeros((1, abi.theta_dim(1, 4, 4)))
+    with pytest.raises(MCPXError):
+        solve_batch(1, 4, 4, tha, linear_solver="schur")  # schur needs the QP family
 
 
 def test_device_api_matches_host_api(gpu):

@@ -33,7 +33,7 @@ def test_oracle_reproduces_golden(oracle_lib, path):
         assert np.all(same), f
 
 
-@pytest.mark.parametrize("ls", ["reduced", "dense"])
+@pytest.mark.parametrize("ls", ["reduced", "dense", "schur"])
 def test_readme_qp_reference_assertions(oracle_lib, ls):
     """test/runtests.jl:30-38 (check_solution) on the README QP (θ = [-0.5, 0.5])."""
     M = np.array([[2.0, 1.0], [1.0, 2.0]]); A = np.eye(2); b = np.ones(2); theta = np.array([-0.5, 0.5])
@@ -66,7 +66,7 @@ def test_game_clamp_reference_assertion(oracle_lib, ls):
 
 @pytest.mark.parametrize("n,m,sp,B,seed", [(16, 8, 0.0, 24, 1), (32, 16, 0.0, 8, 2), (16, 8, 0.9, 8, 3),
                                            (5, 3, 0.3, 24, 4)])
-@pytest.mark.parametrize("ls", ["reduced", "dense"])
+@pytest.mark.parametrize("ls", ["reduced", "dense", "schur"])
 def test_oracle_matches_lapack_restatement(oracle_lib, n, m, sp, B, seed, ls):
     """Independent restatement (numpy + LAPACK getrf on the full system) agrees on
     status / outer / Newton counts and to ≤1e-8 on the iterates."""
@@ -101,6 +101,9 @@ def test_oracle_param_validation(oracle_lib):
                 dict(max_inner_iters=1000), dict(linear_solver=7)):
         with pytest.raises(ValueError):
             oracle_lib.solve_batch(0, 3, 2, th, **bad)
+    tha = np.zeros((1, 4 * 4 + 2 * 4 * 4 + 4 * 4 + 8))
+    with pytest.raises(ValueError):  # schur needs the QP family
+        oracle_lib.solve_batch(1, 4, 4, tha, linear_solver="schur")
 
 
 def test_oracle_threads_deterministic(oracle_lib):

@@ -2,7 +2,7 @@
 // Not a timing build — read the shares, not the absolute time.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -DMCPX_STAMPS=1 \
 //          tools/phase_profile.hip mcp_amd/csrc/mcpx_api.cpp -o tools/phase_profile
-// Run:   tools/phase_profile n m B {spec|gen|gen64|dense}
+// Run:   tools/phase_profile n m B {spec|gen|gen64|dense|schur|schurgen}
 #include "../mcp_amd/csrc/ipm_kernel_impl.hpp"
 
 #include <cstdio>
@@ -55,14 +55,17 @@ int main(int argc, char** argv) {
   for (int k = 0; k <= prm.max_inner_iters; ++k) { a.tight[k] = 1 - exp(-0.1 * k); a.loose[k] = 1 + exp(-0.5 * k); }
   const char* mode = argc > 4 ? argv[4] : "spec";
   a.family = 0;
-  a.reduced = strcmp(mode, "dense") != 0;
+  a.solver = !strcmp(mode, "dense") ? MCPX_LINSOLVE_DENSE
+             : (!strncmp(mode, "schur", 5) ? MCPX_LINSOLVE_SCHUR : MCPX_LINSOLVE_REDUCED);
   for (int rep = 0; rep < 2; ++rep) {
     hipError_t e = hipErrorInvalidValue;
-    if (!strcmp(mode, "spec") && n == 32 && m == 16) e = mcpx::launch_one<48, 0, 32, 16, true>(a, B, 0);
-    else if (!strcmp(mode, "spec") && n == 16 && m == 8) e = mcpx::launch_one<24, 0, 16, 8, true>(a, B, 0);
-    else if (!strcmp(mode, "gen") && n + m <= 48) e = mcpx::launch_one<48, 0, 0, 0, true>(a, B, 0);
-    else if (!strcmp(mode, "gen64")) e = mcpx::launch_one<64, 0, 0, 0, true>(a, B, 0);
-    else if (!strcmp(mode, "dense")) e = mcpx::launch_one<64, 0, 0, 0, false>(a, B, 0);
+    if (!strcmp(mode, "spec") && n == 32 && m == 16) e = mcpx::launch_one<48, 0, 32, 16, MCPX_LINSOLVE_REDUCED>(a, B, 0);
+    else if (!strcmp(mode, "spec") && n == 16 && m == 8) e = mcpx::launch_one<24, 0, 16, 8, MCPX_LINSOLVE_REDUCED>(a, B, 0);
+    else if (!strcmp(mode, "gen") && n + m <= 48) e = mcpx::launch_one<48, 0, 0, 0, MCPX_LINSOLVE_REDUCED>(a, B, 0);
+    else if (!strcmp(mode, "gen64")) e = mcpx::launch_one<64, 0, 0, 0, MCPX_LINSOLVE_REDUCED>(a, B, 0);
+    else if (!strcmp(mode, "dense")) e = mcpx::launch_one<64, 0, 0, 0, MCPX_LINSOLVE_DENSE>(a, B, 0);
+    else if (!strcmp(mode, "schur") && n == 32 && m == 16) e = mcpx::launch_one<32, 0, 32, 16, MCPX_LINSOLVE_SCHUR>(a, B, 0);
+    else if (!strcmp(mode, "schurgen") && n <= 32) e = mcpx::launch_one<32, 0, 0, 0, MCPX_LINSOLVE_SCHUR>(a, B, 0);
     if (e != hipSuccess) { printf("launch failed / unsupported mode: %s\n", hipGetErrorString(e)); return 1; }
     (void)hipDeviceSynchronize();
   }
