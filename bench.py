@@ -6,7 +6,9 @@
 A "step" is one full batched solve (src/solver.jl:35-122 for every instance:
 ϵ-continuation, Newton steps, LU, line search) of B random dense QP-KKT
 instances per GPU (benchmark/quadratic_program_benchmark.jl family, fp64,
-tol = 1e-6 as benchmark/path.jl:8), θ already resident in HBM; with N > 1
+tol = 1e-6 as benchmark/path.jl:8), θ generated on the host (numpy PCG64,
+documented seed) and uploaded before the timed region, so it is
+resident in HBM when timing starts; with N > 1
 ranks each rank solves its own shard (weak scaling: B instances per GPU) and
 the packed per-instance results are all-gathered over RCCL (north_star:
 collective only for solution collection).  Rank 0 prints one JSON line.
@@ -27,6 +29,23 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCP solves/sec (batched QP-KKT, n=64) at 1/2/4/8 GPUs; % LU roofline"
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (AMD datasheet)
+# rocprofv3 PMC pass of this same bench command (tools/gpu_profile.sh), per kernel dispatch
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_c3_schur.json")
+
+
+def pmc_traffic(n: int, m: int, B: int, ls: str):
+    """HBM-side bytes per launch from the committed PMC summary when it was taken on
+    this exact configuration: (FETCH_SIZE + WRITE_SIZE) KB × 1024.  FETCH_SIZE counts
+    L2 misses served by the Infinity Cache too (MI355X_MICROARCH.md, HBM section)."""
+    try:
+        d = json.load(open(PMC_SUMMARY))
+    except (OSError, ValueError):
+        return None, None
+    want = {"schur": 2, "reduced": 0, "dense": 1}[ls]
+    k = d.get("kernel", "")
+    if int(d.get("Grid_Size", 0)) != 64 * B or f", 0, {n}, {m}, {want}>" not in k:
+        return None, None
+    return (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0, os.path.relpath(PMC_SUMMARY, ROOT)
 
 
 def lu_flops(N: int) -> float:
@@ -63,6 +82,8 @@ def parse():
     ap.add_argument("--linear-solver", default="schur", choices=["reduced", "dense", "schur"])
     ap.add_argument("--cpu-sample", type=int, default=32768, help="instances in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--gather", action="store_true",
+                    help="run the RCCL result collection even at world size 1 (rehearsal under torchrun)")
     return ap.parse_args()
 
 
@@ -76,7 +97,13 @@ def cpu_baseline(theta_host: np.ndarray, n: int, m: int, tol: float, threads: in
     t0 = time.perf_counter()
     r = coracle.solve_batch(0, n, m, theta_host, tol=tol, nthreads=threads, linear_solver=ls)
     dt = time.perf_counter() - t0
+    model = ""
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return dict(value=len(theta_host) / dt, unit="solves/s", cores=threads, kind="port",
+                host_cpu=model, host_nproc=os.cpu_count(),
                 sample=f"{len(theta_host)} instances of the same workload (first {len(theta_host)} θ of rank 0), "
                        f"C oracle (oracle/ipm_oracle.c, same algorithm and linear solver) on {threads} host threads, "
                        f"{dt:.2f} s wall = {dt * threads:.1f} thread-s",
@@ -88,48 +115,45 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from mcp_amd.batch import alloc_device_outputs, solve_batch_device
-    from mcp_amd.qp_benchmark import generate_random_parameter_torch
+    from mcp_amd.batch import solve_batch_device
+    from mcp_amd.distributed import Gatherer, alloc_packed
+    from mcp_amd.batch import solve_batch
+    from mcp_amd.qp_benchmark import generate_random_parameter
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    distributed = world > 1 or (a.gather and "RANK" in os.environ)
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("NCCL_DEBUG", "WARN")  # keep RCCL's banner off stdout (one JSON line)
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     n, m, B = a.n, a.m, a.batch
     N = n + 2 * m
 
-    g = torch.Generator(device=dev).manual_seed(a.seed * 1000003 + rank)
-    theta = generate_random_parameter_torch(g, n, m, B, sparsity_rate=a.sparsity, device=dev)
+    # host RNG, one independent stream per rank (SeedSequence(seed, spawn_key=(rank,))), uploaded once
+    rng = np.random.default_rng(np.random.SeedSequence(a.seed, spawn_key=(rank,)))
+    theta_host = generate_random_parameter(rng, n, m, a.sparsity, batch=B)
+    theta = torch.from_numpy(theta_host).to(dev)
     # outputs written straight into one packed fp64 record buffer + one int32 buffer
     # (x | y | s | kkt | ϵ and outer | status | newton), so the collection is 2 all-gathers
-    rec = torch.empty(B * (N + 2), dtype=torch.float64, device=dev)
-    irec = torch.empty(3 * B, dtype=torch.int32, device=dev)
-    out = alloc_device_outputs(B, n, m, dev, newton=True, active=False)
-    o = 0
-    for k, w in (("x", n), ("y", m), ("s", m), ("kkt_error", 1), ("eps", 1)):
-        out[k] = rec[o:o + B * w].view(B, w) if w > 1 else rec[o:o + B]
-        o += B * w
-    out["outer_iters"], out["status"], out["newton_iters"] = irec[:B], irec[B:2 * B], irec[2 * B:]
-    if world > 1:
-        grec = torch.empty(world * rec.numel(), dtype=rec.dtype, device=dev)
-        girec = torch.empty(world * irec.numel(), dtype=irec.dtype, device=dev)
+    packed = alloc_packed(B, n, m, dev)
+    out = packed.views()
+    gather = Gatherer(packed) if distributed else None
 
     stream = torch.cuda.current_stream(dev)
 
     def step():
         solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
-        if world > 1:
-            dist.all_gather_into_tensor(grec, rec)
-            dist.all_gather_into_tensor(girec, irec)
+        if gather is not None:
+            gather()
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     torch.cuda.synchronize(dev)
@@ -138,17 +162,24 @@ def main():
         ev[i][0].record(stream)
         solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
         ev[i][1].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(grec, rec)
-            dist.all_gather_into_tensor(girec, irec)
+        if gather is not None:
+            gather()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    # PCIe-inclusive rate of the host-buffer API (mcpx_solve_batch: H→D θ, solve, D→H
+    # results) — reported beside `value`, never as it
+    host_rate = None
+    if world == 1:
+        solve_batch(0, n, m, theta_host[:1024], tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
+        t1 = time.perf_counter()
+        solve_batch(0, n, m, theta_host, tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
+        host_rate = B / (time.perf_counter() - t1)
     newton = out["newton_iters"].to(torch.float64).sum().item()
     solved = (out["status"] == 0).to(torch.float64).mean().item()
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
@@ -161,6 +192,7 @@ def main():
         # algorithmic FLOPs per Newton step = dense LU of the N = n+2m
         # KKT system, 2N³/3 + 2N², × the run's own Newton counts, per launch (per GPU)
         flops_launch = newton / world * lu_flops(N)
+        traffic, traffic_src = pmc_traffic(n, m, B, a.linear_solver)
         achieved = flops_launch / (kern_ms * 1e-3) / 1e12
         executed = newton / world * executed_flops(n, m, a.linear_solver) / (kern_ms * 1e-3) / 1e12
         res = {
@@ -182,10 +214,12 @@ def main():
                        "n": n, "m": m, "kkt_dim": N, "linear_solver": a.linear_solver, "solve_dim": NS,
                        "batch_per_gpu": B, "global_batch": B * world,
                        "sparsity": a.sparsity,
-                       "parallelism": f"dp{world} (instance shards, RCCL all-gather of results)" if world > 1
+                       "parallelism": f"dp{world} (instance shards, RCCL all-gather of results)" if distributed
                        else "dp1"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes": B * (8 * (n * n + m * n + m + n) + 8 * (n + 2 * m + 2) + 12),
                          "kernel": "ipm_solve_kernel", "kernel_ms": kern_ms,
                          "flops_per_launch": flops_launch,
                          "executed_tflops": executed, "executed_frac": executed / FP64_PEAK_TFLOPS,
@@ -196,13 +230,16 @@ def main():
                                  if a.linear_solver == "schur" else "") + "); FP64 vector = matrix peak on MI355X"},
             "newton_iters_mean": newton / (B * world),
             "success_rate": solved,
+            "host_api_solves_per_s": host_rate,
         }
         if world == 1 and a.cpu_sample > 0:
             th = int(a.cpu_threads) or min(16, os.cpu_count() or 1)
-            res["cpu_baseline"] = cpu_baseline(theta[: a.cpu_sample].cpu().numpy(), n, m, a.tol, th,
-                                               a.linear_solver)
+            res["cpu_baseline"] = cpu_baseline(theta_host[: a.cpu_sample], n, m, a.tol, th, a.linear_solver)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if distributed:
+        if a.gather and world == 1:  # rehearsal: the gathered batch must equal the local results
+            full = gather.unpack()
+            assert all(torch.equal(full[k], packed.views()[k].reshape(full[k].shape)) for k in full)
         dist.destroy_process_group()
 
 
