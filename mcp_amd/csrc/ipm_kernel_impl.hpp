@@ -234,6 +234,66 @@ __device__ __forceinline__ void assemble_row(const double* __restrict__ th, cons
   }
 }
 
+// a[j] ← fma(−l, u_j, a[j]) for j in (k, NMAX) and rhs ← fma(−l, u_rhs, rhs),
+// where u is the row held by the lane(s) in `pm`, broadcast through SGPRs in
+// groups of ≤16 columns (bcast_group.inc).
+template <int NMAX>
+__device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, int k, double l, uint64_t pm) {
+  constexpr int G = 16;  // columns per EXEC-masked broadcast
+  // columns k+1 .. NMAX-1 and the right-hand side (index NMAX)
+#pragma clang loop unroll(full)
+  for (int g = 0; g <= NMAX / G; ++g) {
+    const int lo = max(G * g, k + 1);        // static after unrolling
+    const int hi = min(G * g + G, NMAX + 1);  // exclusive
+    if (lo >= hi) continue;
+    const int cnt = hi - lo;  // 1..16
+    double v[16], u[16];
+#pragma clang loop unroll(full)
+    for (int t = 0; t < 16; ++t) {
+      const int j = lo + t;
+      v[t] = (t < cnt) ? ((j < NMAX) ? a[j < NMAX ? j : 0] : rhs) : 0.0;
+    }
+    bcast_n(cnt, v, pm, u);
+#pragma clang loop unroll(full)
+    for (int t = 0; t < 16; ++t) {
+      const int j = lo + t;
+      if (t < cnt && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
+      if (t < cnt && j == NMAX) rhs = fma(-l, u[t], rhs);
+    }
+  }
+}
+
+// Pivot-free Gauss-Jordan elimination of [S | rhs] for symmetric positive
+// definite S (the SCHUR complement when M is symmetric): pivot k is lane k's
+// row, so there is no pivot search, and every other lane — above and below —
+// eliminates column k.  In a lane-per-row layout the rows above the pivot cost
+// no extra instructions (they were only masked off), and the solution needs no
+// back substitution: x_i = rhs_i / a_ii.  Returns false, leaving a/rhs
+// partially eliminated, as soon as a pivot is not > 0 (not numerically SPD);
+// the caller then falls back to the pivoting LU.  gj_spd_solve() of the oracle.
+template <int NMAX>
+__device__ __forceinline__ bool gj_spd_rows(double (&a)[NMAX], double& rhs, int N, int ln, double& dz) {
+  double dg = 1.0;  // this lane's pivot a_ii
+  bool ok = true;
+#pragma clang loop unroll(full)
+  for (int k = 0; k < NMAX; ++k) {
+    if (k >= N || !ok) continue;  // uniform; no `break` so the loop fully unrolls
+    const double piv = bcast(a[k], k);
+    if (!(piv > 0.0)) {
+      ok = false;
+      continue;
+    }
+    if (ln == k) {
+      dg = piv;
+    } else {
+      eliminate_row<NMAX>(a, rhs, k, a[k] / piv, (uint64_t)opaque64((int64_t)(1ull << k)));
+    }
+  }
+  if (!ok) return false;
+  dz = rhs / dg;
+  return true;
+}
+
 // Dense LU with partial pivoting of the rows held in lanes [0, N) plus the
 // augmented right-hand side, then column-oriented back substitution.  On
 // success returns true and the solution entry of column `ln` in dz; returns
@@ -273,32 +333,7 @@ __device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int
     rem &= ~(1ull << p);
     if (ln == p) my_step = k;
     if (ln == k) pk = p;
-    if ((rem >> ln) & 1ull) {
-      const double l = ak / piv;
-      const uint64_t pm = 1ull << p;
-      constexpr int G = 16;  // columns per EXEC-masked broadcast
-      // columns k+1 .. NMAX-1 and the right-hand side (index NMAX)
-#pragma clang loop unroll(full)
-      for (int g = 0; g <= NMAX / G; ++g) {
-        const int lo = max(G * g, k + 1);        // static after unrolling
-        const int hi = min(G * g + G, NMAX + 1);  // exclusive
-        if (lo >= hi) continue;
-        const int cnt = hi - lo;  // 1..16
-        double v[16], u[16];
-#pragma clang loop unroll(full)
-        for (int t = 0; t < 16; ++t) {
-          const int j = lo + t;
-          v[t] = (t < cnt) ? ((j < NMAX) ? a[j < NMAX ? j : 0] : rhs) : 0.0;
-        }
-        bcast_n(cnt, v, pm, u);
-#pragma clang loop unroll(full)
-        for (int t = 0; t < 16; ++t) {
-          const int j = lo + t;
-          if (t < cnt && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
-          if (t < cnt && j == NMAX) rhs = fma(-l, u[t], rhs);
-        }
-      }
-    }
+    if ((rem >> ln) & 1ull) eliminate_row<NMAX>(a, rhs, k, ak / piv, 1ull << p);
   }
   if (singular) return false;
   dz = 0.0;
@@ -358,6 +393,13 @@ __device__ __forceinline__ void qp_residuals(const double* __restrict__ th, cons
   }
 }
 
+// Lane ln's row of the Schur complement from its LDS tile (zero outside n×n).
+template <int NMAX>
+__device__ __forceinline__ void load_schur_rows(const double* sS, int ln, int n, double (&a)[NMAX]) {
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) a[j] = (ln < n && j < n) ? sS[min(ln, NMAX - 1) * (NMAX + 1) + j] : 0.0;
+}
+
 // SCHUR path, part 2: the n×n Schur complement S = (M + tol·I) + Aᵀ D⁻¹ A on the
 // fp64 matrix cores.  v_mfma_f64_16x16x4_f64 is an ordered fma chain over its
 // 4 k's (tools/ubench_mfma64.hip), so K-chunked accumulation reproduces the
@@ -367,8 +409,8 @@ __device__ __forceinline__ void qp_residuals(const double* __restrict__ th, cons
 // B-fragment holds A_kj / D_k with j = 16J + (l & 15).  The tiles land in LDS
 // (row-major, stride NMAX+1) and each x-lane reads back its row.
 template <int NMAX>
-__device__ __forceinline__ void qp_schur_rows(const double* __restrict__ th, const double* sD, double* sS, int ln,
-                                              int n, int m, double tol, double (&a)[NMAX]) {
+__device__ __forceinline__ void qp_schur_form(const double* __restrict__ th, const double* sD, double* sS, int ln,
+                                              int n, int m, double tol) {
   constexpr int NT = (NMAX + 15) / 16;
   const int nn = n * n;
   const int lr = ln >> 4, lc = ln & 15;
@@ -436,8 +478,6 @@ __device__ __forceinline__ void qp_schur_rows(const double* __restrict__ th, con
         if (row < n && col < n) sS[row * (NMAX + 1) + col] = acc[I][J][r];
       }
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < NMAX; ++j) a[j] = (ln < n && j < n) ? sS[min(ln, NMAX - 1) * (NMAX + 1) + j] : 0.0;
 }
 
 }  // namespace
@@ -452,6 +492,7 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
   __shared__ double zs[64];
   __shared__ double sD[SCH ? 64 : 1], sT[SCH ? 64 : 1];
   __shared__ double sS[SCH ? NMAX * (NMAX + 1) : 1];
+  __shared__ double sB[SCH ? 64 : 1];  // rr, restored for the LU fallback
   const int lane = threadIdx.x;
   const int64_t inst = blockIdx.x;
   const int n0 = NC ? NC : args.n, m0 = MC ? MC : args.m;
@@ -469,6 +510,28 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       if (RED) s = args.s0 ? args.s0[inst * m + (lane - n)] : 1.0;
     }
     if (!RED && lane >= n + m && lane < n + 2 * m) z = args.s0 ? args.s0[inst * m + (lane - n - m)] : 1.0;
+  }
+
+  // SCHUR: M exactly symmetric ⇒ S symmetric ⇒ try the pivot-free SPD
+  // Gauss-Jordan first (oracle: m_sym).  Once per instance.
+  bool spd_try = false;
+  if constexpr (SCH) {
+    const int n = n0;
+    bool asym = false;
+    const int r = min(lane, max(n - 1, 0));
+#pragma clang loop unroll(disable)
+    for (int j0 = 0; j0 < n; j0 += 8) {  // 8 (column, row) pairs in flight
+      double c[8], t[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int j = min(j0 + b, n - 1);
+        c[b] = th0[j * n + r];
+        t[b] = th0[r * n + j];
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) asym |= (lane < n && j0 + b < n) && !(c[b] == t[b]);
+    }
+    spd_try = ballot(asym) == 0ull;
   }
 
   double eps = 1.0;                    // :67
@@ -517,7 +580,7 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       const double kkt_step = any_nan ? __builtin_nan("") : wave_max_nonneg(aF);
       if constexpr (SCH) {
         __syncthreads();
-        qp_schur_rows<NMAX>(th, sD, sS, ln, n, m, tol, a);
+        qp_schur_form<NMAX>(th, sD, sS, ln, n, m, tol);
         // rr_i = −F_Gi + Σ_k A_ki ty_k  (x-lanes; other lanes' value unused)
         rhs = dot_strided<8, false>(th + n * n + (ln < n ? ln : 0) * m, 1, sT, m, rhs);
       }
@@ -527,7 +590,23 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       double dz = 0.0;
       // the LU gets an opaque dimension even in the compile-time kernels: with a
       // constant N the allocator keeps ~40 more VGPRs live (fewer waves/SIMD)
-      const bool ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
+      bool ok = false;
+      if constexpr (SCH) {
+        // S rows come from the LDS tile in both branches, so the fallback LU
+        // never merges two versions of a[] (no phi copies of NMAX registers)
+        sB[ln] = rhs;
+        if (spd_try) {
+          load_schur_rows<NMAX>(sS, ln, n, a);
+          ok = gj_spd_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
+        }
+        if (!ok) {  // M not symmetric, or S not numerically SPD: pivoting LU on the same S
+          load_schur_rows<NMAX>(sS, ln, n, a);
+          rhs = sB[ln];
+          ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
+        }
+      } else {
+        ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
+      }
       MCPX_STAMP(1);
       if (!ok) {
         status = 1;

@@ -38,8 +38,16 @@
  *    ty_k = ry_k / D_k; S_ij = fma chain over k = 0 .. 4⌈m/4⌉−1 starting at
  *    (M_ij + tol·[i=j]) of A_ki · (A_kj / D_k) (k ≥ m contributes fma(0, 0, ·),
  *    the zero padding of the fp64 MFMA K-chunks); rr_i = fma chain over k of
- *    A_ki · ty_k starting at −F_Gi; δx = LU(S) \ rr; δy_k = (fma chain over j
- *    of −A_kj · δx_j starting at ry_k) / D_k; δs as above;
+ *    A_ki · ty_k starting at −F_Gi; δx = S \ rr; δy_k = (fma chain over j
+ *    of −A_kj · δx_j starting at ry_k) / D_k; δs as above.  S \ rr: when M is
+ *    exactly symmetric (checked once per instance), S is symmetric and — if
+ *    every pivot of elimination without pivoting is > 0 — positive definite,
+ *    so it is solved by pivot-free Gauss-Jordan elimination (gj_spd_solve:
+ *    pivot k is row k; every other row i, above and below, is updated with
+ *    l_i = a_ik / a_kk, a_ij ← fma(−l_i, a_kj, a_ij) for j > k and the rhs;
+ *    x_i = b_i / a_ii at the end).  If M is not symmetric or a pivot is not
+ *    > 0 (indefinite / NaN), that Newton step falls back to the partial-
+ *    pivoting LU below on the same S and rr;
  *    (UMFPACK itself, LinearSolve 2.38 UMFPACKFactorization, is a third-party
  *    sparse LU not present here: this dense LU replaces it, results differ in
  *    rounding only);
@@ -209,6 +217,26 @@ static int lu_solve(int N, double* J /* N×N row-major, destroyed */, double* b 
   return 0;
 }
 
+/* Pivot-free Gauss-Jordan on [S | b] for symmetric positive definite S (see the
+ * header); returns 0 ok, 1 when a pivot is not > 0 (caller falls back to lu_solve). */
+static int gj_spd_solve(int n, double* S /* n×n row-major, destroyed */, double* b /* destroyed */,
+                        double* dz) {
+  for (int k = 0; k < n; ++k) {
+    const double piv = S[(size_t)k * n + k];
+    if (!(piv > 0.0)) return 1;
+    const double* u = S + (size_t)k * n;
+    for (int i = 0; i < n; ++i) {
+      if (i == k) continue;
+      double* a = S + (size_t)i * n;
+      const double l = a[k] / piv;
+      for (int j = k + 1; j < n; ++j) a[j] = fma(-l, u[j], a[j]);
+      b[i] = fma(-l, b[k], b[i]);
+    }
+  }
+  for (int i = 0; i < n; ++i) dz[i] = b[i] / S[(size_t)i * n + i];
+  return 0;
+}
+
 /* first e in [0, n_trials) with no violation, or -1 (the NaN of src/solver.jl:131) */
 static int linesearch_exponent(const double* v, const double* d, int cnt, const oracle_tables* t) {
   for (int e = 0; e < t->n_trials; ++e) {
@@ -225,13 +253,15 @@ static int linesearch_exponent(const double* v, const double* d, int cnt, const 
 }
 
 typedef struct ws {
-  double *J, *Jr, *row, *F, *b, *dz, *z, *sD, *sry, *sty;
+  double *J, *Jr, *Js, *bs, *row, *F, *b, *dz, *z, *sD, *sry, *sty;
   int *remaining, *step_of, *prow;
 } ws;
 
 static int ws_alloc(ws* w, int N) {
   w->J = (double*)malloc(sizeof(double) * (size_t)N * N);
   w->Jr = (double*)malloc(sizeof(double) * (size_t)N * N);
+  w->Js = (double*)malloc(sizeof(double) * (size_t)N * N);
+  w->bs = (double*)malloc(sizeof(double) * N);
   w->row = (double*)malloc(sizeof(double) * N);
   w->sD = (double*)malloc(sizeof(double) * N);
   w->sry = (double*)malloc(sizeof(double) * N);
@@ -243,10 +273,10 @@ static int ws_alloc(ws* w, int N) {
   w->remaining = (int*)malloc(sizeof(int) * N);
   w->step_of = (int*)malloc(sizeof(int) * N);
   w->prow = (int*)malloc(sizeof(int) * N);
-  return (w->J && w->Jr && w->sD && w->sry && w->sty && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
+  return (w->J && w->Jr && w->Js && w->bs && w->sD && w->sry && w->sty && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
 }
 static void ws_free(ws* w) {
-  free(w->J); free(w->Jr); free(w->sD); free(w->sry); free(w->sty); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
+  free(w->J); free(w->Jr); free(w->Js); free(w->bs); free(w->sD); free(w->sry); free(w->sty); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
   free(w->remaining); free(w->step_of); free(w->prow);
 }
 
@@ -265,6 +295,13 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
   int status = MCPX_STATUS_SOLVED; /* :69 */
   int outer = 1;              /* :70 */
   int newton = 0;
+  int m_sym = 0; /* SCHUR: M exactly symmetric → try the SPD Gauss-Jordan first */
+  if (p->linear_solver == MCPX_LINSOLVE_SCHUR) {
+    m_sym = 1;
+    for (int i = 0; i < n && m_sym; ++i)
+      for (int j = 0; j < n; ++j)
+        if (!(th[(size_t)j * n + i] == th[(size_t)i * n + j])) { m_sym = 0; break; }
+  }
   while (kkt > p->tol && eps > p->tol && outer < p->max_outer_iters) { /* :71 */
     int inner = 1;            /* :72 */
     status = MCPX_STATUS_SOLVED; /* :73 */
@@ -312,7 +349,13 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           for (int k = 0; k < m; ++k) acc = fma(-w->J[(size_t)i * N + n + k], w->sty[k], acc);
           w->b[i] = acc;
         }
-        if (lu_solve(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
+        int spd_ok = 0;
+        if (m_sym) {
+          memcpy(w->Js, w->Jr, sizeof(double) * (size_t)n * n);
+          memcpy(w->bs, w->b, sizeof(double) * n);
+          spd_ok = gj_spd_solve(n, w->Js, w->bs, w->dz) == 0;
+        }
+        if (!spd_ok && lu_solve(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
           status = MCPX_STATUS_FAILED;
           break;
         }

@@ -60,6 +60,20 @@ def game_clamp_theta(theta, lim=0.5):
     return np.concatenate([P.flatten("F"), Q.flatten("F"), R.flatten("F"), S.flatten("F"), g, h])
 
 
+def qp_theta_with_M(rng, n, m, B, kind):
+    """Random QPs whose M is non-symmetric ("asym": the SCHUR solve falls back to the
+    pivoting LU every step) or symmetric indefinite ("indef": the pivot-free SPD
+    Gauss-Jordan meets a pivot ≤ 0 and that step falls back)."""
+    th = generate_random_parameter(rng, n, m, 0.0, batch=B)
+    M = th[:, :n * n].reshape(B, n, n).transpose(0, 2, 1)  # column-major blocks
+    if kind == "asym":
+        M = M + 0.5 * rng.standard_normal((B, n, n))
+    else:
+        M = M - np.trace(M, axis1=1, axis2=2)[:, None, None] / n * np.eye(n)
+    th[:, :n * n] = M.transpose(0, 2, 1).reshape(B, n * n)
+    return th
+
+
 def case(name, family, n, m, theta, **kw):
     theta = np.atleast_2d(np.asarray(theta, dtype=np.float64))
     r = coracle.solve_batch(family, n, m, theta, trace_len=TRACE, **kw)
@@ -107,6 +121,11 @@ def main():
          tol=1e-6, linear_solver="schur")
     case("qp_n16_m8_sparse_schur", 0, 16, 8,
          generate_random_parameter(np.random.default_rng(3), 16, 8, 0.9, batch=8), tol=1e-6, linear_solver="schur")
+    # the SCHUR solve's fallback from the SPD Gauss-Jordan to the pivoting LU
+    case("qp_n16_m8_asym_schur", 0, 16, 8, qp_theta_with_M(np.random.default_rng(4), 16, 8, 8, "asym"), tol=1e-6,
+         linear_solver="schur")
+    case("qp_n16_m8_indef_schur", 0, 16, 8, qp_theta_with_M(np.random.default_rng(5), 16, 8, 8, "indef"), tol=1e-6,
+         linear_solver="schur")
 
 
 if __name__ == "__main__":

@@ -105,6 +105,23 @@ def test_random_qp_vs_oracle(gpu, oracle_lib, n, m, sp, B, seed, ls):
     assert_parity(got, ref)
 
 
+@pytest.mark.parametrize("kind", ["asym", "indef"])
+@pytest.mark.parametrize("n,m,B,seed", [(16, 8, 64, 31), (32, 16, 32, 32), (9, 5, 64, 33), (24, 20, 32, 34)])
+@pytest.mark.parametrize("variant", ["specialized", "generic"])
+def test_schur_fallback_vs_oracle(gpu, oracle_lib, kind, n, m, B, seed, variant, monkeypatch):
+    """Non-symmetric M (the SCHUR solve never tries the SPD Gauss-Jordan) and symmetric
+    indefinite M (Gauss-Jordan meets a pivot ≤ 0 and the step falls back to the LU)."""
+    from tests.golden.make_golden import qp_theta_with_M
+
+    if variant == "generic":
+        monkeypatch.setenv("MCPX_GENERIC_KERNELS", "1")
+    theta = qp_theta_with_M(np.random.default_rng(seed), n, m, B, kind)
+    kw = dict(tol=1e-6, linear_solver="schur", max_outer_iters=12)
+    got = solve_batch(0, n, m, theta, trace_len=TRACE, **kw)
+    ref = oracle_lib.solve_batch(0, n, m, theta, trace_len=TRACE, **kw)
+    assert_parity(got, ref)
+
+
 @pytest.mark.parametrize("ls", ["reduced", "dense"])
 def test_affine_family_vs_oracle(gpu, oracle_lib, ls):
     rng = np.random.default_rng(5)
