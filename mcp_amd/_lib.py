@@ -12,7 +12,8 @@ import os
 from . import _abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmcpx.so")
+# MCPX_LIB_PATH: load an alternative in-tree build (kernel A/B experiments, tools/)
+LIB_PATH = os.environ.get("MCPX_LIB_PATH") or os.path.join(_HERE, "libmcpx.so")
 _lib = None
 
 

@@ -39,14 +39,16 @@ def _stale() -> bool:
     return any(os.path.getmtime(p) > t for p in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None) -> str:
+    """`out`: alternative output path (kernel A/B variants built with `extra_flags`)."""
+    lib_path = out or LIB
+    if out is None and not force and not _stale():
         return LIB
     t0 = time.time()
     objs, procs = [], []
     jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 1)
     for src in SOURCES:  # one hipcc per translation unit, `jobs` at a time
-        obj = os.path.join(CSRC, os.path.basename(src) + ".o")
+        obj = os.path.join(CSRC, os.path.basename(src) + (".alt" if out else "") + ".o")
         cmd = [HIPCC, *FLAGS, *extra_flags, "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -57,14 +59,14 @@ def build(force: bool = False, verbose: bool = False, extra_flags=()) -> str:
     for p, src in zip(procs, SOURCES):
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, f"hipcc {src}")
-    tmp = LIB + ".tmp"
+    tmp = lib_path + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib_path)
     for o in objs:
         os.remove(o)
     if verbose:
-        print(f"built {LIB} in {time.time() - t0:.1f}s", flush=True)
-    return LIB
+        print(f"built {lib_path} in {time.time() - t0:.1f}s", flush=True)
+    return lib_path
 
 
 if __name__ == "__main__":

@@ -283,6 +283,11 @@ __device__ __forceinline__ bool gj_spd_rows(double (&a)[NMAX], double& rhs, int 
       ok = false;
       continue;
     }
+    // pivot row through SGPRs (EXEC-masked readfirstlane).  The static pivot lane
+    // would allow an LDS broadcast instead (one VALU op per element less), but
+    // its store→load→fma latency chain per step measured 1.45× slower at C3.
+    // The mask is re-materialised per step (opaque): hoisted, the 32 constant
+    // masks would occupy 64 SGPRs and spill.
     if (ln == k) {
       dg = piv;
     } else {
