@@ -485,6 +485,295 @@ __device__ __forceinline__ void qp_schur_form(const double* __restrict__ th, con
   __syncthreads();
 }
 
+// ---- 2-D Gauss-Jordan on the matrix-core output layout (SCHUR, SPD) --------
+//
+// The Schur complement is formed transposed on the matrix cores (the A fragment
+// carries A_kj / D_k, the B fragment A_ki, the accumulator starts at Mᵀ), so
+// that accumulator tile (I, J), element r of lane (lr, lc) = (l >> 4, l & 15)
+// holds S[16J + lc][16I + lr + 4r]: lane (lr, lc) owns rows lc + 16J of S at
+// the columns ≡ lr (mod 4), and every DPP row of 16 lanes holds all rows.
+// (fma(a, b, c) = fma(b, a, c), so every entry is bit-identical to the oracle's
+// S_ij chain.)  In this layout a Gauss-Jordan step needs the pivot row's entry
+// of the lane's own column — one DPP row_newbcast source operand of the fma —
+// and two row multipliers per lane, moved across DPP rows with
+// v_permlane16/32_swap.  Compared with the lane-per-row layout this replaces
+// two v_readfirstlane + one fma per element by one v_fmac_f64_dpp, keeps S in
+// NT²·8 instead of 32·NT·2 VGPRs, and needs no LDS round trip of the tile.
+
+// v from DPP row Q (lanes 16Q .. 16Q+15) in every DPP row, lane position kept:
+// v_permlane16_swap replicates the even / odd DPP rows, v_permlane32_swap the
+// lower / upper half (semantics checked by tools/ubench_lanes.hip).  Written as
+// inline asm so that it stays ordered after the asm fmacs of the previous step,
+// with the wait states for reading their results that the compiler cannot see
+// (FIRST: the step right after the MFMAs, whose results need more).
+template <int Q, bool FIRST>
+__device__ __forceinline__ double from_dpp_row(double v) {
+  unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  unsigned a0, a1, b0, b1, c0, c1, d0, d1;
+#define MCPX_PL_STAGE1(SEL_LO, SEL_HI)                                                     \
+  "v_mov_b32 %0, %8\n v_mov_b32 %1, %8\n v_mov_b32 %2, %9\n v_mov_b32 %3, %9\n s_nop 1\n" \
+  "v_permlane16_swap_b32 %0, %1\n v_permlane16_swap_b32 %2, %3\n s_nop 1\n"              \
+  "v_mov_b32 %4, " SEL_LO "\n v_mov_b32 %5, " SEL_LO "\n"                                \
+  "v_mov_b32 %6, " SEL_HI "\n v_mov_b32 %7, " SEL_HI "\n s_nop 1\n"                     \
+  "v_permlane32_swap_b32 %4, %5\n v_permlane32_swap_b32 %6, %7\n s_nop 1"
+#define MCPX_PL_ASM(PRE, SEL_LO, SEL_HI)                                                   \
+  asm volatile(PRE MCPX_PL_STAGE1(SEL_LO, SEL_HI)                                          \
+               : "=&v"(a0), "=&v"(a1), "=&v"(b0), "=&v"(b1), "=&v"(c0), "=&v"(c1), "=&v"(d0), \
+                 "=&v"(d1)                                                                 \
+               : "v"(lo), "v"(hi))
+  if (FIRST) {
+    if (Q & 1) MCPX_PL_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%1", "%3");
+    else MCPX_PL_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%0", "%2");
+  } else {
+    if (Q & 1) MCPX_PL_ASM("s_nop 4\n", "%1", "%3");
+    else MCPX_PL_ASM("s_nop 4\n", "%0", "%2");
+  }
+#undef MCPX_PL_ASM
+#undef MCPX_PL_STAGE1
+  // c0/d0: lower half replicated (Q < 2), c1/d1: upper half replicated (Q ≥ 2)
+  return (Q & 2) ? __hiloint2double((int)d1, (int)c1) : __hiloint2double((int)d0, (int)c0);
+}
+
+// (v_permlane*_swap reads its operands 2 wait states after a VALU write at the
+// earliest: the s_nop 1 ahead of each swap in the asm blocks.)
+//
+// NT = 2: both row halves' multipliers with ONE division.  v0 / v1 = the pivot
+// column entries of half 0 / 1, valid in DPP row Q.  permlane32_swap puts half
+// 0's values in the lower and half 1's in the upper 32 lanes (same DPP-row
+// offset), permlane16_swap then spreads DPP row Q within each half, so lane l
+// holds w = a_{16·(l≥32) + lc, k}; one division gives t = w / piv, and a final
+// permlane32_swap hands every lane both t's (lower → half 0, upper → half 1).
+template <int Q, bool FIRST>
+__device__ __forceinline__ void col_quot_nt2(double v0, double v1, double piv, double& q0, double& q1) {
+  unsigned w[2];
+  const unsigned s0[2] = {(unsigned)__double2loint(v0), (unsigned)__double2hiint(v0)};
+  const unsigned s1[2] = {(unsigned)__double2loint(v1), (unsigned)__double2hiint(v1)};
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    unsigned x, y, z;
+#define MCPX_NT2_ASM(PRE, SEL, OTHER_IS_X)                                                         \
+  asm volatile(PRE "v_mov_b32 %0, %3\n v_mov_b32 %1, %4\n s_nop 1\n v_permlane32_swap_b32 %0, %1\n"  \
+               "s_nop 1\n v_mov_b32 %2, " SEL "\n s_nop 1\n v_permlane16_swap_b32 " SEL ", %2\n s_nop 1" \
+               : "=&v"(x), "=&v"(y), "=&v"(z) : "v"(s0[t]), "v"(s1[t]))
+    // rows 0/1 of half 0 and 1 sit in x (Q < 2), rows 2/3 in y (Q ≥ 2); after the
+    // 16-swap SEL holds the even DPP rows replicated and z the odd ones
+    if (FIRST) {
+      if (Q < 2) MCPX_NT2_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%0", 1);
+      else MCPX_NT2_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%1", 0);
+    } else {
+      if (Q < 2) MCPX_NT2_ASM("s_nop 4\n", "%0", 1);
+      else MCPX_NT2_ASM("s_nop 4\n", "%1", 0);
+    }
+#undef MCPX_NT2_ASM
+    w[t] = (Q & 1) ? z : ((Q < 2) ? x : y);
+  }
+  const double t = __hiloint2double((int)w[1], (int)w[0]) / piv;
+  const unsigned tl = (unsigned)__double2loint(t), thi = (unsigned)__double2hiint(t);
+  const auto pl = __builtin_amdgcn_permlane32_swap(tl, tl, false, false);
+  const auto ph = __builtin_amdgcn_permlane32_swap(thi, thi, false, false);
+  q0 = __hiloint2double((int)ph[0], (int)pl[0]);  // lower half replicated: half 0
+  q1 = __hiloint2double((int)ph[1], (int)pl[1]);  // upper half replicated: half 1
+}
+
+// acc ← fma(nl, u, acc), u = lane (16·row + R)'s `src` (DPP row_newbcast:R).
+// The DPP source is the pivot row, last written one step earlier: the column
+// distribution and the division lie between (≥ 2 wait states).
+#define MCPX_FMAC_NB(R)                                                                      \
+  case R:                                                                                    \
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"  \
+                 : "+v"(acc) : "v"(src), "v"(nl));                                           \
+    break;
+template <int R>
+__device__ __forceinline__ void fmac_row_bcast(double& acc, double src, double nl) {
+  switch (R) {
+    MCPX_FMAC_NB(0) MCPX_FMAC_NB(1) MCPX_FMAC_NB(2) MCPX_FMAC_NB(3) MCPX_FMAC_NB(4) MCPX_FMAC_NB(5)
+    MCPX_FMAC_NB(6) MCPX_FMAC_NB(7) MCPX_FMAC_NB(8) MCPX_FMAC_NB(9) MCPX_FMAC_NB(10) MCPX_FMAC_NB(11)
+    MCPX_FMAC_NB(12) MCPX_FMAC_NB(13) MCPX_FMAC_NB(14) MCPX_FMAC_NB(15)
+  }
+}
+#undef MCPX_FMAC_NB
+
+// Same with the destination as its own DPP source (the pivot half; a DPP read
+// happens before the write, so every lane sees the pivot lane's old value).
+#define MCPX_FMAC_NB_SELF(R)                                                                 \
+  case R:                                                                                    \
+    asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"  \
+                 : "+v"(acc) : "v"(nl));                                                     \
+    break;
+template <int R>
+__device__ __forceinline__ void fmac_row_bcast_self(double& acc, double nl) {
+  switch (R) {
+    MCPX_FMAC_NB_SELF(0) MCPX_FMAC_NB_SELF(1) MCPX_FMAC_NB_SELF(2) MCPX_FMAC_NB_SELF(3) MCPX_FMAC_NB_SELF(4)
+    MCPX_FMAC_NB_SELF(5) MCPX_FMAC_NB_SELF(6) MCPX_FMAC_NB_SELF(7) MCPX_FMAC_NB_SELF(8) MCPX_FMAC_NB_SELF(9)
+    MCPX_FMAC_NB_SELF(10) MCPX_FMAC_NB_SELF(11) MCPX_FMAC_NB_SELF(12) MCPX_FMAC_NB_SELF(13)
+    MCPX_FMAC_NB_SELF(14) MCPX_FMAC_NB_SELF(15)
+  }
+}
+#undef MCPX_FMAC_NB_SELF
+
+// Transposed Schur complement in the 2-D layout (see above).  acc[I][J][r].
+template <int NT>
+__device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, const double* sD, int ln, int n,
+                                                 int m, double tol, d4 (&acc)[NT][NT]) {
+  const int lr = ln >> 4, lc = ln & 15;
+  {  // C = Mᵀ blocks: element (p = lr + 4r, q = lc) of tile (I, J) is M[16J+q][16I+p] = θ[(16I+p)·n + 16J+q]
+    double mv[NT][NT][4];
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = 0; J < NT; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int col = min(16 * I + lr + 4 * r, n - 1), row = min(16 * J + lc, n - 1);
+          mv[I][J][r] = th[col * n + row];
+        }
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = 0; J < NT; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int col = 16 * I + lr + 4 * r, row = 16 * J + lc;
+          const bool in = row < n && col < n;
+          const double v = mv[I][J][r];
+          acc[I][J][r] = in ? (row == col ? v + tol : v) : 0.0;  // M_ij (+ tol on the diagonal)
+        }
+  }
+  const int nn = n * n;
+  const int kc = (m + 3) / 4;
+  double nxt[NT];
+#pragma unroll
+  for (int X = 0; X < NT; ++X) nxt[X] = th[nn + min(16 * X + lc, n - 1) * m + min(lr, max(m - 1, 0))];
+  for (int c = 0; c < kc; ++c) {
+    const int k = 4 * c + lr;
+    const bool kin = k < m;
+    const double dk = sD[kin ? k : 0];
+    double cur[NT];
+#pragma unroll
+    for (int X = 0; X < NT; ++X) cur[X] = nxt[X];
+    if (c + 1 < kc) {
+      const int k1 = min(k + 4, m - 1);
+#pragma unroll
+      for (int X = 0; X < NT; ++X) nxt[X] = th[nn + min(16 * X + lc, n - 1) * m + k1];
+    }
+    double af[NT], bf[NT];
+#pragma unroll
+    for (int X = 0; X < NT; ++X) {
+      const bool in = kin && 16 * X + lc < n;
+      af[X] = in ? cur[X] / dk : 0.0;  // A_kj / D_k   (j = 16I + p)
+      bf[X] = in ? cur[X] : 0.0;       // A_ki         (i = 16J + q)
+    }
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = 0; J < NT; ++J) acc[I][J] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[I], bf[J], acc[I][J], 0, 0, 0);
+  }
+}
+
+// Pivot-free Gauss-Jordan of [S | rh] in the 2-D layout; gj_spd_solve() of the
+// oracle step for step (pivot k = row k; rows ≠ k: l = a_ik / a_kk,
+// a_ij ← fma(−l, a_kj, a_ij) for j > k, rh_i ← fma(−l, rh_k, rh_i); then the
+// pivot row a_kj ← fma(a_kj, +0, a_kj), rh_k likewise; x_i = rh_i / a_ii).  Entries of columns ≤ k are also touched in a lane
+// whose local column block straddles k; those are never read again.
+// rh[J] / x[J]: row 16J + lc, replicated over the four DPP rows.
+template <int NT>
+__device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[NT], int N, int ln, double (&x)[NT]) {
+  const int lc = ln & 15;
+  double dg[NT];
+#pragma unroll
+  for (int J = 0; J < NT; ++J) dg[J] = 1.0;
+  bool ok = true;
+#pragma clang loop unroll(full)
+  for (int k = 0; k < 16 * NT; ++k) {
+    if (k >= N || !ok) continue;
+    const int Jk = k >> 4, Rk = k & 15;        // pivot row 16·Jk + Rk
+    const int Qk = k & 3, Ck = k >> 2;         // pivot column: DPP row Qk, local column Ck
+    const int Ik = Ck >> 2, rk = Ck & 3;       // local column Ck = accumulator tile Ik, element rk
+    const double piv = bcast(acc[Ik][Jk][rk], 16 * Qk + Rk);
+    if (!(piv > 0.0)) {
+      ok = false;
+      continue;
+    }
+    const bool prow = lc == Rk;  // this lane holds the pivot row in half Jk
+    if (prow) dg[Jk] = piv;
+    double nl[NT];
+    if constexpr (NT == 2) {
+      double q0, q1;
+      switch (Qk + (k == 0 ? 4 : 0)) {  // static after unrolling
+        case 0: col_quot_nt2<0, false>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
+        case 1: col_quot_nt2<1, false>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
+        case 2: col_quot_nt2<2, false>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
+        case 3: col_quot_nt2<3, false>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
+        default: col_quot_nt2<0, true>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
+      }
+      nl[0] = -q0;  // −l: the fma takes −l · u exactly as fma(−l, u, a)
+      nl[1] = -q1;
+    } else {
+#pragma unroll
+      for (int J = 0; J < NT; ++J) {
+        double colv;
+        const bool first = k == 0 && J == 0;
+        switch (Qk + (first ? 4 : 0)) {  // static after unrolling
+          case 0: colv = from_dpp_row<0, false>(acc[Ik][J][rk]); break;
+          case 1: colv = from_dpp_row<1, false>(acc[Ik][J][rk]); break;
+          case 2: colv = from_dpp_row<2, false>(acc[Ik][J][rk]); break;
+          case 3: colv = from_dpp_row<3, false>(acc[Ik][J][rk]); break;
+          default: colv = from_dpp_row<0, true>(acc[Ik][J][rk]); break;  // k = 0: DPP row 0
+        }
+        nl[J] = -(colv / piv);
+      }
+    }
+    // The pivot row takes the same fma with multiplier +0 (a_kj ← fma(a_kj, +0, a_kj),
+    // mirrored by the oracle): masking its lanes off instead would make them
+    // invalid DPP sources for the other lanes of the pivot half.
+    if (prow) nl[Jk] = 0.0;
+#pragma unroll
+    for (int J = 0; J < NT; ++J) {
+      if (J == Jk) continue;  // the pivot half last
+#pragma unroll
+      for (int c = 0; c < 4 * NT; ++c) {
+        if (4 * c + 3 <= k) continue;  // every column of this local block ≤ k
+        switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast<R>(acc[c >> 2][J][c & 3], acc[c >> 2][Jk][c & 3], nl[J]); break;
+          MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+          MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14)
+          MCPX_CASE(15)
+#undef MCPX_CASE
+        }
+      }
+      switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast<R>(rh[J], rh[Jk], nl[J]); break;
+        MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+        MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14) MCPX_CASE(15)
+#undef MCPX_CASE
+      }
+    }
+    {  // half Jk (pivot lanes: multiplier +0), after the other halves have read the pivot row
+#pragma unroll
+      for (int c = 0; c < 4 * NT; ++c) {
+        if (4 * c + 3 <= k) continue;
+        switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast_self<R>(acc[c >> 2][Jk][c & 3], nl[Jk]); break;
+          MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+          MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14)
+          MCPX_CASE(15)
+#undef MCPX_CASE
+        }
+      }
+      switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast_self<R>(rh[Jk], nl[Jk]); break;
+        MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+        MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14) MCPX_CASE(15)
+#undef MCPX_CASE
+      }
+    }
+  }
+  if (!ok) return false;
+#pragma unroll
+  for (int J = 0; J < NT; ++J) x[J] = rh[J] / dg[J];
+  return true;
+}
+
 }  // namespace
 
 // NC, MC > 0: compile-time (n, m) specialisation; 0: runtime n, m.
@@ -585,9 +874,9 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       const double kkt_step = any_nan ? __builtin_nan("") : wave_max_nonneg(aF);
       if constexpr (SCH) {
         __syncthreads();
-        qp_schur_form<NMAX>(th, sD, sS, ln, n, m, tol);
         // rr_i = −F_Gi + Σ_k A_ki ty_k  (x-lanes; other lanes' value unused)
         rhs = dot_strided<8, false>(th + n * n + (ln < n ? ln : 0) * m, 1, sT, m, rhs);
+        sB[ln] = rhs;
       }
       MCPX_STAMP(0);
 
@@ -597,14 +886,29 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       // constant N the allocator keeps ~40 more VGPRs live (fewer waves/SIMD)
       bool ok = false;
       if constexpr (SCH) {
-        // S rows come from the LDS tile in both branches, so the fallback LU
-        // never merges two versions of a[] (no phi copies of NMAX registers)
-        sB[ln] = rhs;
-        if (spd_try) {
-          load_schur_rows<NMAX>(sS, ln, n, a);
-          ok = gj_spd_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
+        constexpr int NT = (NMAX + 15) / 16;
+        if (spd_try) {  // S formed transposed on the matrix cores, Gauss-Jordan in that layout
+          d4 acc4[NT][NT];
+          qp_schur_form_2d<NT>(th, sD, ln, n, m, tol, acc4);
+          double acc[NT][NT][4];
+#pragma unroll
+          for (int I = 0; I < NT; ++I)
+#pragma unroll
+            for (int J = 0; J < NT; ++J)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[I][J][r] = acc4[I][J][r];
+          __syncthreads();  // rr (sB) of every row
+          double rh2[NT], x2[NT];
+#pragma unroll
+          for (int J = 0; J < NT; ++J) rh2[J] = (16 * J + (ln & 15) < n) ? sB[16 * J + (ln & 15)] : 0.0;
+          ok = gj2d_spd<NT>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, x2);
+#pragma unroll
+          for (int J = 0; J < NT; ++J)
+            if ((ln >> 4) == J) dz = x2[J];  // lane 16J + lc owns row 16J + lc
         }
         if (!ok) {  // M not symmetric, or S not numerically SPD: pivoting LU on the same S
+          __syncthreads();
+          qp_schur_form<NMAX>(th, sD, sS, ln, n, m, tol);
           load_schur_rows<NMAX>(sS, ln, n, a);
           rhs = sB[ln];
           ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
@@ -622,7 +926,10 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
         zs[ln] = dz;
         __syncthreads();
         const double acc = dot_strided<8, true>(th + n * n + (rh ? ln - n : 0), m, zs, n, ryr);
-        if (rh) dz = acc / D;
+        // branch-free consumer: under `if (rh)` the compiler sinks all n loads of
+        // the dot into that block at once (n more live registers)
+        const double dzy = acc / D;
+        dz = rh ? dzy : dz;
       }
       double ds = 0.0;
       if (RED && rh) ds = fma(-s, dz, -Fc) / w;  // δs_k = (−F_Ck − s_k δy_k) / w_k

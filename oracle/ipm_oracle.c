@@ -44,8 +44,9 @@
  *    every pivot of elimination without pivoting is > 0 — positive definite,
  *    so it is solved by pivot-free Gauss-Jordan elimination (gj_spd_solve:
  *    pivot k is row k; every other row i, above and below, is updated with
- *    l_i = a_ik / a_kk, a_ij ← fma(−l_i, a_kj, a_ij) for j > k and the rhs;
- *    x_i = b_i / a_ii at the end).  If M is not symmetric or a pivot is not
+ *    l_i = a_ik / a_kk, a_ij ← fma(−l_i, a_kj, a_ij) for j > k and the rhs,
+ *    then the pivot row itself a_kj ← fma(a_kj, +0, a_kj) (identity unless
+ *    non-finite; the GPU updates every lane uniformly); x_i = b_i / a_ii).  If M is not symmetric or a pivot is not
  *    > 0 (indefinite / NaN), that Newton step falls back to the partial-
  *    pivoting LU below on the same S and rr;
  *    (UMFPACK itself, LinearSolve 2.38 UMFPACKFactorization, is a third-party
@@ -232,6 +233,11 @@ static int gj_spd_solve(int n, double* S /* n×n row-major, destroyed */, double
       for (int j = k + 1; j < n; ++j) a[j] = fma(-l, u[j], a[j]);
       b[i] = fma(-l, b[k], b[i]);
     }
+    /* the pivot row takes the same update with multiplier +0 (the GPU's lane-uniform
+       update; identity for finite entries, Inf → NaN otherwise) */
+    double* a = S + (size_t)k * n;
+    for (int j = k + 1; j < n; ++j) a[j] = fma(a[j], 0.0, a[j]);
+    b[k] = fma(b[k], 0.0, b[k]);
   }
   for (int i = 0; i < n; ++i) dz[i] = b[i] / S[(size_t)i * n + i];
   return 0;
