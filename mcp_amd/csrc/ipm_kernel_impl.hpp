@@ -503,9 +503,9 @@ __device__ __forceinline__ void qp_schur_form(const double* __restrict__ th, con
 // v from DPP row Q (lanes 16Q .. 16Q+15) in every DPP row, lane position kept:
 // v_permlane16_swap replicates the even / odd DPP rows, v_permlane32_swap the
 // lower / upper half (semantics checked by tools/ubench_lanes.hip).  Written as
-// inline asm so that it stays ordered after the asm fmacs of the previous step,
-// with the wait states for reading their results that the compiler cannot see
-// (FIRST: the step right after the MFMAs, whose results need more).
+// inline asm so that it stays ordered after the asm fmacs of the previous step
+// (FIRST: the step right after the MFMAs, whose results need wait states before
+// a VALU read that the compiler cannot see through the asm).
 template <int Q, bool FIRST>
 __device__ __forceinline__ double from_dpp_row(double v) {
   unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
@@ -525,8 +525,8 @@ __device__ __forceinline__ double from_dpp_row(double v) {
     if (Q & 1) MCPX_PL_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%1", "%3");
     else MCPX_PL_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%0", "%2");
   } else {
-    if (Q & 1) MCPX_PL_ASM("s_nop 4\n", "%1", "%3");
-    else MCPX_PL_ASM("s_nop 4\n", "%0", "%2");
+    if (Q & 1) MCPX_PL_ASM("", "%1", "%3");
+    else MCPX_PL_ASM("", "%0", "%2");
   }
 #undef MCPX_PL_ASM
 #undef MCPX_PL_STAGE1
@@ -545,29 +545,30 @@ __device__ __forceinline__ double from_dpp_row(double v) {
 // permlane32_swap hands every lane both t's (lower → half 0, upper → half 1).
 template <int Q, bool FIRST>
 __device__ __forceinline__ void col_quot_nt2(double v0, double v1, double piv, double& q0, double& q1) {
-  unsigned w[2];
-  const unsigned s0[2] = {(unsigned)__double2loint(v0), (unsigned)__double2hiint(v0)};
-  const unsigned s1[2] = {(unsigned)__double2loint(v1), (unsigned)__double2hiint(v1)};
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    unsigned x, y, z;
-#define MCPX_NT2_ASM(PRE, SEL, OTHER_IS_X)                                                         \
-  asm volatile(PRE "v_mov_b32 %0, %3\n v_mov_b32 %1, %4\n s_nop 1\n v_permlane32_swap_b32 %0, %1\n"  \
-               "s_nop 1\n v_mov_b32 %2, " SEL "\n s_nop 1\n v_permlane16_swap_b32 " SEL ", %2\n s_nop 1" \
-               : "=&v"(x), "=&v"(y), "=&v"(z) : "v"(s0[t]), "v"(s1[t]))
-    // rows 0/1 of half 0 and 1 sit in x (Q < 2), rows 2/3 in y (Q ≥ 2); after the
-    // 16-swap SEL holds the even DPP rows replicated and z the odd ones
-    if (FIRST) {
-      if (Q < 2) MCPX_NT2_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%0", 1);
-      else MCPX_NT2_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%1", 0);
-    } else {
-      if (Q < 2) MCPX_NT2_ASM("s_nop 4\n", "%0", 1);
-      else MCPX_NT2_ASM("s_nop 4\n", "%1", 0);
-    }
-#undef MCPX_NT2_ASM
-    w[t] = (Q & 1) ? z : ((Q < 2) ? x : y);
+  const unsigned a0 = (unsigned)__double2loint(v0), a1 = (unsigned)__double2hiint(v0);
+  const unsigned b0 = (unsigned)__double2loint(v1), b1 = (unsigned)__double2hiint(v1);
+  unsigned x0, y0, z0, x1, y1, z1;  // per dword (0 = low, 1 = high)
+  // rows 0/1 of half 0 and 1 end up in x (Q < 2), rows 2/3 in y (Q ≥ 2); after the
+  // 16-swap the selected register holds the even DPP rows replicated, z the odd ones.
+  // Both dword chains interleaved, so each swap's wait states overlap the other's.
+#define MCPX_NT2_ASM(PRE, S0, S1)                                                                      \
+  asm volatile(PRE "v_mov_b32 %0, %6\n v_mov_b32 %1, %7\n v_mov_b32 %3, %8\n v_mov_b32 %4, %9\n"     \
+               "s_nop 1\n v_permlane32_swap_b32 %0, %1\n v_permlane32_swap_b32 %3, %4\n s_nop 0\n"   \
+               "v_mov_b32 %2, " S0 "\n v_mov_b32 %5, " S1 "\n s_nop 1\n"                              \
+               "v_permlane16_swap_b32 " S0 ", %2\n v_permlane16_swap_b32 " S1 ", %5\n s_nop 1"         \
+               : "=&v"(x0), "=&v"(y0), "=&v"(z0), "=&v"(x1), "=&v"(y1), "=&v"(z1)                     \
+               : "v"(a0), "v"(b0), "v"(a1), "v"(b1))
+  if (FIRST) {  // right after the MFMAs: their results need more wait states before a VALU read
+    if (Q < 2) MCPX_NT2_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%0", "%3");
+    else MCPX_NT2_ASM("s_nop 7\n s_nop 7\n s_nop 7\n", "%1", "%4");
+  } else {
+    if (Q < 2) MCPX_NT2_ASM("", "%0", "%3");
+    else MCPX_NT2_ASM("", "%1", "%4");
   }
-  const double t = __hiloint2double((int)w[1], (int)w[0]) / piv;
+#undef MCPX_NT2_ASM
+  const unsigned w0 = (Q & 1) ? z0 : ((Q < 2) ? x0 : y0);
+  const unsigned w1 = (Q & 1) ? z1 : ((Q < 2) ? x1 : y1);
+  const double t = __hiloint2double((int)w1, (int)w0) / piv;
   const unsigned tl = (unsigned)__double2loint(t), thi = (unsigned)__double2hiint(t);
   const auto pl = __builtin_amdgcn_permlane32_swap(tl, tl, false, false);
   const auto ph = __builtin_amdgcn_permlane32_swap(thi, thi, false, false);
