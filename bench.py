@@ -207,8 +207,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (random dense QPs of benchmark/quadratic_program_benchmark.jl, torch Philox seed "
-                    f"{a.seed}+rank, generated in HBM)",
+            "data": "synthetic (random dense QPs of benchmark/quadratic_program_benchmark.jl, host numpy PCG64 "
+                    f"SeedSequence({a.seed}, spawn_key=(rank,)), uploaded to HBM before timing)",
             "config": {"workload": f"BASELINE C3: random dense QP-KKT n={n} m={m} (KKT dim {N}), fp64, "
                                    f"{B} instances per GPU, tol={a.tol:g}",
                        "n": n, "m": m, "kkt_dim": N, "linear_solver": a.linear_solver, "solve_dim": NS,
