@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MCPX_VERSION 10000 /* 1.0.0 */
+#define MCPX_VERSION 10100 /* 1.1.0 */
 
 /* error codes */
 #define MCPX_OK 0
@@ -161,6 +161,50 @@ int mcpx_solve_batch_device(const mcpx_desc* desc, const double* theta,
                             const double* x0, const double* y0, const double* s0,
                             const mcpx_params* prm, const mcpx_out* out,
                             void* stream);
+
+
+/* ---------------------------------------------------------------------------
+ * Sensitivities of a solution w.r.t. θ (reference src/AutoDiff.jl).
+ *
+ * The reference differentiates F(z; θ) = 0 at the returned iterate:
+ *     ∂z/∂θ = −(∇F_z)⁻¹ ∇F_θ      (src/AutoDiff.jl:18-40; `qr(−∇F_z, ColumnNorm()) \ ∇F_θ`)
+ * with ∇F_z WITHOUT the tol·I regularisation, at the final (x, y, s)
+ * (SURVEY.md Appendix A.10).  For both families ∇F_z and ∇F_θ do not depend on ϵ.
+ * The kernels solve the same square system by dense LU with partial pivoting
+ * of the full (n+2m)-dim ∇F_z (or its transpose); for a nonsingular ∇F_z that
+ * equals the reference's pivoted-QR solve up to rounding.  An exactly zero
+ * pivot (∇F_z singular, where the reference's QR would return a basic
+ * least-squares solution) is reported per instance: status[b] = 1 and the
+ * instance's outputs are NaN.
+ *
+ * Reverse mode — the ChainRulesCore.rrule pullback (src/AutoDiff.jl:42-82):
+ *     ∂θ = (∂z/∂θ)ᵀ [∂l/∂x; ∂l/∂y; ∂l/∂s] = −∇F_θᵀ λ,  ∇F_zᵀ λ = [∂l/∂x; ∂l/∂y; ∂l/∂s].
+ * Inputs (instance-major): θ (stride theta_ld), x [B*n], y [B*m], s [B*m],
+ * gx [B*n], gy [B*m], gs [B*m] (any of gx/gy/gs may be NULL = zero cotangent,
+ * ChainRulesCore's ZeroTangent).  Output: dtheta [B*p] (p = mcpx_theta_dim,
+ * dense stride p, the family's θ layout), status [B] or NULL.
+ * Needs n + 2m <= MCPX_MAX_KKT_DIM. */
+int mcpx_vjp_batch(const mcpx_desc* desc, const double* theta, const double* x, const double* y,
+                   const double* s, const double* gx, const double* gy, const double* gs,
+                   int num_devices, double* dtheta, int32_t* status);
+/* Same on device buffers of the current device, enqueued on `stream`. */
+int mcpx_vjp_batch_device(const mcpx_desc* desc, const double* theta, const double* x,
+                          const double* y, const double* s, const double* gx, const double* gy,
+                          const double* gs, double* dtheta, int32_t* status, void* stream);
+
+/* Forward mode — the ForwardDiff.Dual method of solve (src/AutoDiff.jl:84-117):
+ *     ż_c = (∂z/∂θ) θ̇_c = −(∇F_z)⁻¹ (∇F_θ θ̇_c),   c = 0 .. n_partials−1.
+ * theta_dot [B*n_partials*p] (instance-major, then partial-major, stride p);
+ * zdot [B*n_partials*(n+2m)], z = [x; y; s] ordering (src/mcp.jl:74);
+ * status [B] or NULL.  One factorisation of ∇F_z serves up to
+ * MCPX_JVP_RHS partials at a time. */
+#define MCPX_JVP_RHS 8
+int mcpx_jvp_batch(const mcpx_desc* desc, const double* theta, const double* x, const double* y,
+                   const double* s, int32_t n_partials, const double* theta_dot, int num_devices,
+                   double* zdot, int32_t* status);
+int mcpx_jvp_batch_device(const mcpx_desc* desc, const double* theta, const double* x,
+                          const double* y, const double* s, int32_t n_partials,
+                          const double* theta_dot, double* zdot, int32_t* status, void* stream);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,7 @@ FAMILY_QP = 0
 FAMILY_AFFINE = 1
 
 MAX_KKT_DIM = 64
+JVP_RHS = 8  # MCPX_JVP_RHS: partials per factorisation of the JVP kernel
 
 LINSOLVE_REDUCED = 0
 LINSOLVE_DENSE = 1

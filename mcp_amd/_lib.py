@@ -26,7 +26,8 @@ class MCPXError(RuntimeError):
 
 
 EXPORTS = ("mcpx_version", "mcpx_last_error", "mcpx_default_params", "mcpx_theta_dim",
-           "mcpx_device_count", "mcpx_solve_batch", "mcpx_solve_batch_device")
+           "mcpx_device_count", "mcpx_solve_batch", "mcpx_solve_batch_device", "mcpx_vjp_batch",
+           "mcpx_vjp_batch_device", "mcpx_jvp_batch", "mcpx_jvp_batch_device")
 
 
 def lib():
@@ -51,6 +52,15 @@ def lib():
     L.mcpx_solve_batch_device.argtypes = [C.POINTER(_abi.Desc), C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_void_p, C.POINTER(_abi.Params), C.POINTER(_abi.Out),
                                           C.c_void_p]
+    P = C.c_void_p
+    L.mcpx_vjp_batch.restype = C.c_int
+    L.mcpx_vjp_batch.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, P, P, P, C.c_int, P, P]
+    L.mcpx_vjp_batch_device.restype = C.c_int
+    L.mcpx_vjp_batch_device.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, P, P, P, P, P, P]
+    L.mcpx_jvp_batch.restype = C.c_int
+    L.mcpx_jvp_batch.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, C.c_int, P, P]
+    L.mcpx_jvp_batch_device.restype = C.c_int
+    L.mcpx_jvp_batch_device.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, P, P, P]
     _lib = L
     return L
 

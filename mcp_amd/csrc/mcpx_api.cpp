@@ -20,6 +20,7 @@
 
 #include "../../include/mcpx.h"
 #include "ipm_kernel.h"
+#include "sens_kernel.h"
 
 namespace {
 
@@ -225,6 +226,124 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   return MCPX_OK;
 }
 
+
+// ---- sensitivities (src/AutoDiff.jl) ----------------------------------------
+
+// Validates a sensitivity call; fills the scalar part of the args and the kernel width.
+int prepare_sens(const mcpx_desc* d, mcpx::SensArgs* a, int* nmax) {
+  if (!d) return fail(MCPX_EINVAL, "desc must be non-NULL");
+  const int64_t pd = mcpx_theta_dim(d->family, d->n, d->m);
+  if (pd < 0) return fail(MCPX_EINVAL, "bad family %d or negative dimensions (n=%d, m=%d)", d->family, d->n, d->m);
+  if (d->n + d->m < 1) return fail(MCPX_EINVAL, "empty problem (n = m = 0)");
+  if (d->batch < 0) return fail(MCPX_EINVAL, "negative batch");
+  if (d->theta_ld < pd) return fail(MCPX_EINVAL, "theta_ld %lld < parameter dimension %lld", (long long)d->theta_ld, (long long)pd);
+  const int N = d->n + 2 * d->m;
+  *nmax = pick_nmax(N);
+  if (*nmax < 0 || N > MCPX_MAX_KKT_DIM)
+    return fail(MCPX_EUNSUPPORTED, "sensitivities need n + 2m <= %d (got n=%d m=%d)", MCPX_MAX_KKT_DIM, d->n, d->m);
+  std::memset(a, 0, sizeof *a);
+  a->theta_ld = d->theta_ld;
+  a->p = pd;
+  a->n = d->n;
+  a->m = d->m;
+  a->family = d->family;
+  return MCPX_OK;
+}
+
+// Enqueue VJP (jvp = false) or JVP launches over the batch in chunks of 2^30 instances.
+int launch_sens(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, int nmax, const double* theta, const double* x,
+                const double* y, const double* s, const double* gx, const double* gy, const double* gs,
+                const double* tdot, double* out, int32_t* status, hipStream_t st) {
+  const int64_t CH = (int64_t)1 << 30;
+  const int n = d->n, m = d->m, N = n + 2 * m, K = a.n_partials;
+  for (int64_t b0 = 0; b0 < d->batch; b0 += CH) {
+    const int64_t nb = std::min(CH, d->batch - b0);
+    a.theta = theta + b0 * d->theta_ld;
+    a.x = x + b0 * n;
+    a.y = y + b0 * m;
+    a.s = s + b0 * m;
+    a.gx = gx ? gx + b0 * n : nullptr;
+    a.gy = gy ? gy + b0 * m : nullptr;
+    a.gs = gs ? gs + b0 * m : nullptr;
+    a.theta_dot = tdot ? tdot + b0 * K * a.p : nullptr;
+    a.out = out + (jvp ? b0 * K * N : b0 * a.p);
+    a.status = status ? status + b0 : nullptr;
+    HIP_TRY(jvp ? mcpx::launch_jvp(nmax, a, nb, st) : mcpx::launch_vjp(nmax, a, nb, st));
+  }
+  return MCPX_OK;
+}
+
+// One device's share [b0, b0+nb) of a host-buffer sensitivity call.
+int sens_shard(bool jvp, int dev, const mcpx_desc* d, const mcpx::SensArgs& a0, int nmax, const double* theta,
+               const double* x, const double* y, const double* s, const double* gx, const double* gy,
+               const double* gs, const double* tdot, double* out, int32_t* status, int64_t b0, int64_t nb) {
+  HIP_TRY(hipSetDevice(dev));
+  int rc = check_device(dev);
+  if (rc) return rc;
+  const int n = d->n, m = d->m, N = n + 2 * m, K = a0.n_partials;
+  const int64_t p = a0.p;
+  DevBuf<double> th, dx, dy, ds, dgx, dgy, dgs, dtd, dout;
+  DevBuf<int32_t> dst;
+  auto up = [&](DevBuf<double>& b, const double* h, size_t per) -> hipError_t {
+    if (!h || !per || !nb) return hipSuccess;
+    hipError_t e = b.alloc((size_t)nb * per);
+    return e != hipSuccess ? e : hipMemcpy(b.p, h + b0 * per, sizeof(double) * nb * per, hipMemcpyHostToDevice);
+  };
+  HIP_TRY(up(th, theta, (size_t)d->theta_ld));
+  HIP_TRY(up(dx, x, n)); HIP_TRY(up(dy, y, m)); HIP_TRY(up(ds, s, m));
+  HIP_TRY(up(dgx, gx, n)); HIP_TRY(up(dgy, gy, m)); HIP_TRY(up(dgs, gs, m));
+  HIP_TRY(up(dtd, tdot, (size_t)K * p));
+  const size_t per_out = jvp ? (size_t)K * N : (size_t)p;
+  HIP_TRY(dout.alloc((size_t)nb * per_out));
+  if (status) HIP_TRY(dst.alloc(nb));
+  mcpx_desc dd = *d;
+  dd.batch = nb;
+  // empty x/y blocks (n = 0 or m = 0) still need a valid base pointer
+  const double* bx = dx.p ? dx.p : th.p;
+  const double* by = dy.p ? dy.p : th.p;
+  const double* bs = ds.p ? ds.p : th.p;
+  if ((rc = launch_sens(jvp, &dd, a0, nmax, th.p, bx, by, bs, gx ? dgx.p : nullptr, gy ? dgy.p : nullptr,
+                        gs ? dgs.p : nullptr, dtd.p, dout.p, status ? dst.p : nullptr, nullptr)))
+    return rc;
+  HIP_TRY(hipDeviceSynchronize());
+  if (per_out) HIP_TRY(hipMemcpy(out + b0 * per_out, dout.p, sizeof(double) * nb * per_out, hipMemcpyDeviceToHost));
+  if (status) HIP_TRY(hipMemcpy(status + b0, dst.p, sizeof(int32_t) * nb, hipMemcpyDeviceToHost));
+  return MCPX_OK;
+}
+
+// Host-buffer entry shared by mcpx_vjp_batch / mcpx_jvp_batch: contiguous shards, one thread per device.
+int sens_host(bool jvp, const mcpx_desc* d, const mcpx::SensArgs& a, int nmax, const double* theta,
+              const double* x, const double* y, const double* s, const double* gx, const double* gy,
+              const double* gs, const double* tdot, int num_devices, double* out, int32_t* status) {
+  const int avail = mcpx_device_count();
+  if (avail < 1) return fail(MCPX_ENODEV, "no HIP device visible");
+  if (num_devices <= 0 || num_devices > avail) num_devices = avail;
+  if ((int64_t)num_devices > d->batch) num_devices = (int)d->batch;
+  std::vector<int64_t> start(num_devices + 1, 0);
+  for (int g = 0; g < num_devices; ++g)
+    start[g + 1] = start[g] + d->batch / num_devices + (g < d->batch % num_devices ? 1 : 0);
+  std::vector<int> rcs(num_devices, 0);
+  std::vector<std::string> errs(num_devices);
+  std::vector<std::thread> th;
+  for (int g = 0; g < num_devices; ++g)
+    th.emplace_back([&, g] {
+      rcs[g] = sens_shard(jvp, g, d, a, nmax, theta, x, y, s, gx, gy, gs, tdot, out, status, start[g],
+                          start[g + 1] - start[g]);
+      if (rcs[g]) errs[g] = g_err;
+    });
+  for (auto& t : th) t.join();
+  for (int g = 0; g < num_devices; ++g)
+    if (rcs[g]) return fail(rcs[g], "device %d: %s", g, errs[g].c_str());
+  return MCPX_OK;
+}
+
+int sens_inputs_ok(const mcpx_desc* d, const double* theta, const double* x, const double* y, const double* s,
+                   const double* out) {
+  if (!theta || !out) return fail(MCPX_EINVAL, "theta and the output array must be non-NULL");
+  if ((d->n > 0 && !x) || (d->m > 0 && (!y || !s))) return fail(MCPX_EINVAL, "solution arrays x/y/s must be non-NULL");
+  return MCPX_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -304,6 +423,64 @@ int mcpx_solve_batch(const mcpx_desc* d, const double* theta, const double* x0, 
   for (int g = 0; g < num_devices; ++g)
     if (rcs[g]) return fail(rcs[g], "device %d: %s", g, errs[g].c_str());
   return MCPX_OK;
+}
+
+int mcpx_vjp_batch_device(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                          const double* s, const double* gx, const double* gy, const double* gs, double* dtheta,
+                          int32_t* status, void* stream) {
+  mcpx::SensArgs a;
+  int nmax, rc;
+  if ((rc = prepare_sens(d, &a, &nmax))) return rc;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, dtheta))) return rc;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if ((rc = check_device(dev))) return rc;
+  return launch_sens(false, d, a, nmax, theta, x ? x : theta, y ? y : theta, s ? s : theta, gx, gy, gs, nullptr,
+                     dtheta, status, (hipStream_t)stream);
+}
+
+int mcpx_vjp_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y, const double* s,
+                   const double* gx, const double* gy, const double* gs, int num_devices, double* dtheta,
+                   int32_t* status) {
+  mcpx::SensArgs a;
+  int nmax, rc;
+  if ((rc = prepare_sens(d, &a, &nmax))) return rc;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, dtheta))) return rc;
+  return sens_host(false, d, a, nmax, theta, x, y, s, gx, gy, gs, nullptr, num_devices, dtheta, status);
+}
+
+int mcpx_jvp_batch_device(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                          const double* s, int32_t n_partials, const double* theta_dot, double* zdot,
+                          int32_t* status, void* stream) {
+  mcpx::SensArgs a;
+  int nmax, rc;
+  if ((rc = prepare_sens(d, &a, &nmax))) return rc;
+  if (n_partials < 0) return fail(MCPX_EINVAL, "negative n_partials");
+  a.n_partials = n_partials;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, zdot))) return rc;
+  if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if ((rc = check_device(dev))) return rc;
+  return launch_sens(true, d, a, nmax, theta, x ? x : theta, y ? y : theta, s ? s : theta, nullptr, nullptr,
+                     nullptr, theta_dot, zdot, status, (hipStream_t)stream);
+}
+
+int mcpx_jvp_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y, const double* s,
+                   int32_t n_partials, const double* theta_dot, int num_devices, double* zdot, int32_t* status) {
+  mcpx::SensArgs a;
+  int nmax, rc;
+  if ((rc = prepare_sens(d, &a, &nmax))) return rc;
+  if (n_partials < 0) return fail(MCPX_EINVAL, "negative n_partials");
+  a.n_partials = n_partials;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, zdot))) return rc;
+  if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
+  return sens_host(true, d, a, nmax, theta, x, y, s, nullptr, nullptr, nullptr, theta_dot, num_devices, zdot,
+                   status);
 }
 
 }  // extern "C"

@@ -1,0 +1,331 @@
+// sens_kernel_impl.hpp — gfx950 kernels of the solution sensitivities
+// (reference src/AutoDiff.jl).  Instantiated by sens_inst_vjp.hip / sens_inst_jvp.hip.
+//
+// The reference differentiates F(z; θ) = 0 at the returned iterate (x, y, s):
+//     ∂z/∂θ = −(∇F_z)⁻¹ ∇F_θ           (src/AutoDiff.jl:18-40, pivoted QR of −∇F_z)
+// with ∇F_z taken WITHOUT the solver's tol·I (src/AutoDiff.jl:25-31).
+//
+//  * vjp_kernel — the rrule pullback (src/AutoDiff.jl:42-82):
+//        ∂θ = (∂z/∂θ)ᵀ g = −∇F_θᵀ λ,   ∇F_zᵀ λ = g = [∂l/∂x; ∂l/∂y; ∂l/∂s].
+//    Lane j owns row j of ∇F_zᵀ (= column j of ∇F_z) plus g_j; the register LU of
+//    the Newton step (lu_solve_rows, ipm_kernel_impl.hpp) solves for λ, which
+//    goes to LDS with z; ∂θ is then written as coalesced rank-1 blocks
+//    (∂M = −λ_x xᵀ, ∂A_kj = λ_x,j y_k − λ_y,k x_j, ∂b = λ_y, ∂ϕ = λ_x for the QP
+//    family; −λ ⊗ z blocks for the affine family).
+//  * jvp_kernel — the ForwardDiff.Dual method (src/AutoDiff.jl:84-117):
+//        ż_c = −(∇F_z)⁻¹ (∇F_θ θ̇_c)  for K partials.
+//    Lane i owns row i of ∇F_z plus up to R right-hand sides −(∇F_θ θ̇_c)_i; one
+//    LU of ∇F_z serves R partials (lu_solve_rows_multi).
+//
+// One 64-lane wave per instance, as the solver.  The ∇F_z rows are assembled
+// straight from θ in registers (no Jacobian in HBM).  Arithmetic follows
+// oracle_vjp_batch / oracle_jvp_batch of oracle/ipm_oracle.c op for op, so the
+// results are bit-identical to the oracle.
+#pragma once
+
+#include "ipm_kernel_impl.hpp"
+#include "sens_kernel.h"
+
+namespace mcpx {
+namespace {
+
+// Row `ln` of ∇F_z (TR = false) or of ∇F_zᵀ (TR = true) at z = zs (LDS:
+// x at 0, y at n, s at n+m), WITHOUT tol·I (src/AutoDiff.jl:27-31).  Entries of
+// the x-column block (j < n) are ±px[j·sx], of the y-column block ±py[(j−n)·sy];
+// the θ-independent entries (−I, diag(s), diag(y), src/mcp.jl:76-80) are the two
+// (c1, v1), (c2, v2) pairs.  `RowPattern` is reused by the JVP right-hand side
+// (the same θ pattern applied to a tangent θ̇).
+struct RowPattern {
+  int64_t ox, oy;  // offsets of the row's x / y column blocks in θ
+  int sx, sy;      // strides (0 with use = false)
+  bool usex, usey, negx, negy;
+  int c1, c2;
+  double v1, v2;
+};
+
+template <int FAMILY, bool TR>
+__device__ __forceinline__ RowPattern row_pattern(const double* zs, int ln, int n, int m) {
+  const int N = n + 2 * m;
+  const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m;
+  const bool lx = ln < n, ly = ln >= n && ln < n + m, lz = ln >= n + m && ln < N;
+  const int q = ln - n, r = ln - n - m;
+  RowPattern P{0, 0, 0, 0, false, false, false, false, -1, -1, 0.0, 0.0};
+  if (!TR) {  // row ln of ∇F_z = [[M, −Aᵀ, 0], [A, 0, −I], [0, diag(s), diag(y)]] (QP)
+    if (lx) {
+      P.usex = true; P.ox = ln; P.sx = n;                       // M[i,j] / P[i,j] = θ[j·n + i]
+      P.usey = true;
+      if (FAMILY == 0) { P.oy = nn + (int64_t)ln * m; P.sy = 1; P.negy = true; }  // −A[k,i]
+      else { P.oy = nn + ln; P.sy = n; }                        // Q[i,k] = θ[n² + k·n + i]
+    }
+    if (ly) {
+      P.usex = true; P.sx = m;
+      P.ox = (FAMILY == 0 ? nn : nn + nm) + q;                  // A[q,j] / R[q,j]
+      if (FAMILY != 0) { P.usey = true; P.oy = nn + 2 * nm + q; P.sy = m; }  // S[q,l]
+      P.c1 = n + m + q; P.v1 = -1.0;                            // ∂(H − s)/∂s = −I
+    }
+    if (lz) {
+      P.c1 = n + r; P.v1 = zs[n + m + r];                       // ∂(s⊙y)/∂y = diag(s)
+      P.c2 = n + m + r; P.v2 = zs[n + r];                       // ∂(s⊙y)/∂s = diag(y)
+    }
+  } else {  // row ln of ∇F_zᵀ = column ln of ∇F_z
+    if (lx) {
+      P.usex = true; P.ox = (int64_t)ln * n; P.sx = 1;          // M[i,ln] / P[i,ln]
+      P.usey = true; P.sy = 1;
+      P.oy = (FAMILY == 0 ? nn : nn + nm) + (int64_t)ln * m;    // A[k,ln] / R[k,ln]
+    }
+    if (ly) {
+      P.usex = true;
+      if (FAMILY == 0) { P.ox = nn + q; P.sx = m; P.negx = true; }  // −A[q,i]
+      else { P.ox = nn + (int64_t)q * n; P.sx = 1; }                // Q[i,q]
+      if (FAMILY != 0) { P.usey = true; P.oy = nn + 2 * nm + (int64_t)q * m; P.sy = 1; }  // S[k,q]
+      P.c1 = n + m + q; P.v1 = zs[n + m + q];                   // ∂(s⊙y)_q/∂y_q = s_q
+    }
+    if (lz) {
+      P.c1 = n + r; P.v1 = -1.0;                                // ∂(H − s)_r/∂s_r
+      P.c2 = n + m + r; P.v2 = zs[n + r];                       // ∂(s⊙y)_r/∂s_r = y_r
+    }
+  }
+  return P;
+}
+
+template <int NMAX>
+__device__ __forceinline__ void assemble_pattern_row(const double* __restrict__ th, const RowPattern& P, int n,
+                                                     int m, double (&a)[NMAX]) {
+  const double* px = th + (P.usex ? P.ox : 0);
+  const double* py = th + (P.usey ? P.oy : 0);
+  const int sx = P.usex ? P.sx : 0, sy = P.usey ? P.sy : 0;
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) {
+    double v = 0.0;
+    if (j < n) {
+      const double t = px[j * sx];
+      if (P.usex) v = P.negx ? -t : t;
+    } else if (j < n + m) {
+      const double t = py[(j - n) * sy];
+      if (P.usey) v = P.negy ? -t : t;
+    }
+    if (j == P.c1) v = P.v1;
+    if (j == P.c2) v = P.v2;
+    a[j] = v;
+  }
+}
+
+// (∇F_θ θ̇)_ln for the row pattern of ∇F_z (TR = false) applied to the tangent
+// θ̇: the x-block chain, then the y-block chain, then the θ-only term
+// (QP: −ϕ̇_i / −ḃ_q, affine: +ġ_i / +ḣ_q); complementarity rows: 0.
+// fma_chain order of oracle dtheta_row().
+template <int FAMILY>
+__device__ __forceinline__ double dtheta_row(const double* __restrict__ d, const RowPattern& P, const double* zs,
+                                             int ln, int n, int m) {
+  const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
+  double acc = 0.0;
+  if (P.usex)
+    for (int j = 0; j < n; ++j) {
+      const double t = d[P.ox + (int64_t)j * P.sx];
+      acc = fma(P.negx ? -t : t, zs[j], acc);
+    }
+  if (P.usey)
+    for (int k = 0; k < m; ++k) {
+      const double t = d[P.oy + (int64_t)k * P.sy];
+      acc = fma(P.negy ? -t : t, zs[n + k], acc);
+    }
+  if (ln < n) return FAMILY == 0 ? acc - d[nn + nm + m + ln] : acc + d[nn + 2 * nm + mm + ln];
+  if (ln < n + m) return FAMILY == 0 ? acc - d[nn + nm + (ln - n)] : acc + d[nn + 2 * nm + mm + n + (ln - n)];
+  return 0.0;
+}
+
+// a[j] ← fma(−l, u_j, a[j]) for j in (k, NMAX) and r[c] ← fma(−l, u_{NMAX+c}, r[c]):
+// eliminate_row() of the solver, widened to R right-hand sides.
+template <int NMAX, int R>
+__device__ __forceinline__ void eliminate_row_multi(double (&a)[NMAX], double (&r)[R], int k, double l,
+                                                    uint64_t pm) {
+  constexpr int G = 16;
+  constexpr int W = NMAX + R;
+#pragma clang loop unroll(full)
+  for (int g = 0; g <= (W - 1) / G; ++g) {
+    const int lo = max(G * g, k + 1);
+    const int hi = min(G * g + G, W);
+    if (lo >= hi) continue;
+    const int cnt = hi - lo;
+    double v[16], u[16];
+#pragma clang loop unroll(full)
+    for (int t = 0; t < 16; ++t) {
+      const int j = lo + t;
+      v[t] = (t < cnt) ? ((j < NMAX) ? a[j < NMAX ? j : 0] : r[j >= NMAX && j - NMAX < R ? j - NMAX : 0]) : 0.0;
+    }
+    bcast_n(cnt, v, pm, u);
+#pragma clang loop unroll(full)
+    for (int t = 0; t < 16; ++t) {
+      const int j = lo + t;
+      if (t < cnt && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
+      if (t < cnt && j >= NMAX) r[j - NMAX < R ? j - NMAX : 0] = fma(-l, u[t], r[j - NMAX < R ? j - NMAX : 0]);
+    }
+  }
+}
+
+// lu_solve_rows() with R right-hand sides: same pivot rule (first remaining row
+// of largest |a_ik|, NaN never wins), same elimination and back substitution
+// per right-hand side, so every column equals the single-rhs solve bitwise.
+template <int NMAX, int R>
+__device__ __forceinline__ bool lu_solve_rows_multi(double (&a)[NMAX], double (&r)[R], int N, int ln,
+                                                    double (&dz)[R]) {
+  uint64_t rem = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
+  int my_step = 1 << 30;
+  int pk = 0;
+  bool singular = false;
+#pragma clang loop unroll(full)
+  for (int k = 0; k < NMAX; ++k) {
+    if (k >= N || singular) continue;
+    const double ak = a[k];
+    const double av = fabs(ak);
+    const bool valid = ((rem >> ln) & 1ull) && !(av != av);
+    const uint32_t khi = valid ? (uint32_t)__double2hiint(av) + 1u : 0u;
+    const uint32_t mhi = wave_max_u32(khi);
+    int p;
+    if (mhi == 0u) {
+      p = lowest_lane(rem);
+    } else {
+      const uint64_t cand = ballot(khi == mhi);
+      if (__popcll(cand) == 1) {
+        p = lowest_lane(cand);
+      } else {
+        const uint32_t klo = (khi == mhi) ? (uint32_t)__double2loint(av) : 0u;
+        const uint32_t mlo = wave_max_u32(klo);
+        p = lowest_lane(ballot(khi == mhi && klo == mlo));
+      }
+    }
+    const double piv = bcast(ak, p);
+    if (piv == 0.0) {
+      singular = true;
+      continue;
+    }
+    rem &= ~(1ull << p);
+    if (ln == p) my_step = k;
+    if (ln == k) pk = p;
+    if ((rem >> ln) & 1ull) eliminate_row_multi<NMAX, R>(a, r, k, ak / piv, 1ull << p);
+  }
+  if (singular) return false;
+#pragma unroll
+  for (int c = 0; c < R; ++c) dz[c] = 0.0;
+#pragma clang loop unroll(full)
+  for (int k = NMAX - 1; k >= 0; --k) {
+    if (k < N) {
+      const int p = __builtin_amdgcn_readlane(pk, k);
+      const double akk = a[k];
+#pragma unroll
+      for (int c = 0; c < R; ++c) {
+        const double xk = bcast(r[c] / akk, p);
+        if (ln == k) dz[c] = xk;
+        if (my_step < k) r[c] = fma(-akk, xk, r[c]);
+      }
+    }
+  }
+  return true;
+}
+
+// out[t] = f(row, col) for t = row + rows·col < rows·cols, 64 lanes at a time
+// (coalesced stores of a column-major block).
+template <class Fn>
+__device__ __forceinline__ void write_block(double* __restrict__ out, int rows, int cols, int ln, Fn f) {
+  const int total = rows * cols;
+  if (total <= 0) return;
+  int r = ln % rows, c = ln / rows;
+  const int dr = 64 % rows, dc = 64 / rows;
+  for (int t = ln; t < total; t += 64) {
+    out[t] = f(r, c);
+    r += dr;
+    c += dc;
+    if (r >= rows) {
+      r -= rows;
+      ++c;
+    }
+  }
+}
+
+// Load z = [x; y; s] of instance `inst` into LDS (zs[0, n+2m)).
+__device__ __forceinline__ void load_z(const SensArgs& A, int64_t inst, int ln, double* zs) {
+  const int n = A.n, m = A.m;
+  double v = 0.0;
+  if (ln < n) v = A.x[inst * n + ln];
+  else if (ln < n + m) v = A.y[inst * m + (ln - n)];
+  else if (ln < n + 2 * m) v = A.s[inst * m + (ln - n - m)];
+  zs[ln] = v;
+}
+
+template <int NMAX, int FAMILY>
+__global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
+  __shared__ double zs[64];
+  __shared__ double lam[64];
+  const int ln = threadIdx.x;
+  const int64_t inst = blockIdx.x;
+  const int n = A.n, m = A.m, N = n + 2 * m;
+  const double* th = A.theta + inst * A.theta_ld;
+  load_z(A, inst, ln, zs);
+  __syncthreads();
+  double a[NMAX];
+  const RowPattern P = row_pattern<FAMILY, true>(zs, ln, n, m);
+  assemble_pattern_row<NMAX>(th, P, n, m, a);
+  double g = 0.0;  // ∂l/∂z_ln (NULL cotangent block = ZeroTangent)
+  if (ln < n) { if (A.gx) g = A.gx[inst * n + ln]; }
+  else if (ln < n + m) { if (A.gy) g = A.gy[inst * m + (ln - n)]; }
+  else if (ln < N) { if (A.gs) g = A.gs[inst * m + (ln - n - m)]; }
+  double l = 0.0;
+  const bool ok = lu_solve_rows<NMAX>(a, g, N, ln, l);
+  lam[ln] = ok ? l : __builtin_nan("");
+  __syncthreads();
+  if (A.status && ln == 0) A.status[inst] = ok ? 0 : 1;
+  double* o = A.out + inst * A.p;
+  const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
+  const double* x = zs;
+  const double* y = zs + n;
+  const double* lx = lam;      // λ of the G rows
+  const double* ly = lam + n;  // λ of the H − s rows
+  if (FAMILY == 0) {
+    write_block(o, n, n, ln, [&](int i, int j) { return -(lx[i] * x[j]); });               // ∂M_ij
+    write_block(o + nn, m, n, ln, [&](int k, int j) { return fma(lx[j], y[k], -(ly[k] * x[j])); });  // ∂A_kj
+    write_block(o + nn + nm, m, 1, ln, [&](int k, int) { return ly[k]; });                 // ∂b_k
+    write_block(o + nn + nm + m, n, 1, ln, [&](int i, int) { return lx[i]; });             // ∂ϕ_i
+  } else {
+    write_block(o, n, n, ln, [&](int i, int j) { return -(lx[i] * x[j]); });               // ∂P_ij
+    write_block(o + nn, n, m, ln, [&](int i, int k) { return -(lx[i] * y[k]); });          // ∂Q_ik
+    write_block(o + nn + nm, m, n, ln, [&](int k, int j) { return -(ly[k] * x[j]); });     // ∂R_kj
+    write_block(o + nn + 2 * nm, m, m, ln, [&](int k, int q) { return -(ly[k] * y[q]); }); // ∂S_kq
+    write_block(o + nn + 2 * nm + mm, n, 1, ln, [&](int i, int) { return -lx[i]; });       // ∂g_i
+    write_block(o + nn + 2 * nm + mm + n, m, 1, ln, [&](int k, int) { return -ly[k]; });   // ∂h_k
+  }
+}
+
+template <int NMAX, int FAMILY>
+__global__ __launch_bounds__(64) void jvp_kernel(const SensArgs A) {
+  constexpr int R = MCPX_JVP_RHS;
+  __shared__ double zs[64];
+  const int ln = threadIdx.x;
+  const int64_t inst = blockIdx.x;
+  const int n = A.n, m = A.m, N = n + 2 * m, K = A.n_partials;
+  const double* th = A.theta + inst * A.theta_ld;
+  load_z(A, inst, ln, zs);
+  __syncthreads();
+  const RowPattern P = row_pattern<FAMILY, false>(zs, ln, n, m);
+  bool all_ok = true;
+  for (int c0 = 0; c0 < K; c0 += R) {  // one factorisation of ∇F_z per R partials
+    double a[NMAX], r[R], dz[R];
+    assemble_pattern_row<NMAX>(th, P, n, m, a);
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      r[c] = 0.0;
+      if (c0 + c < K) {
+        const double* d = A.theta_dot + (inst * K + c0 + c) * A.p;
+        r[c] = -dtheta_row<FAMILY>(d, P, zs, ln, n, m);
+      }
+    }
+    const bool ok = lu_solve_rows_multi<NMAX, R>(a, r, N, ln, dz);
+    all_ok = all_ok && ok;
+#pragma unroll
+    for (int c = 0; c < R; ++c)
+      if (c0 + c < K && ln < N) A.out[(inst * K + c0 + c) * N + ln] = ok ? dz[c] : __builtin_nan("");
+  }
+  if (A.status && ln == 0) A.status[inst] = all_ok ? 0 : 1;
+}
+
+}  // namespace
+}  // namespace mcpx

@@ -74,3 +74,54 @@ def solve_batch(family: int, n: int, m: int, theta: np.ndarray, *, x0=None, y0=N
     if rc != 0:
         raise ValueError(f"oracle_solve_batch failed with code {rc}")
     return r
+
+
+def _sens_lib():
+    L = lib()
+    if not hasattr(L, "_sens_ready"):
+        L.oracle_vjp_batch.restype = C.c_int
+        L.oracle_vjp_batch.argtypes = [C.POINTER(Desc)] + [C.c_void_p] * 9 + [C.c_int]
+        L.oracle_jvp_batch.restype = C.c_int
+        L.oracle_jvp_batch.argtypes = [C.POINTER(Desc), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L._sens_ready = True
+    return L
+
+
+def _f64(a, shape):
+    return None if a is None else np.ascontiguousarray(np.broadcast_to(a, shape), dtype=np.float64)
+
+
+def vjp_batch(family: int, n: int, m: int, theta, x, y, s, gx=None, gy=None, gs=None, nthreads: int = 1):
+    """Oracle of mcpx_vjp_batch: returns (dtheta (B, p), status (B,))."""
+    theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+    B, ld = theta.shape
+    p = theta_dim(family, n, m)
+    x, y, s = _f64(x, (B, n)), _f64(y, (B, m)), _f64(s, (B, m))
+    gx, gy, gs = _f64(gx, (B, n)), _f64(gy, (B, m)), _f64(gs, (B, m))
+    dth = np.empty((B, p))
+    st = np.empty(B, np.int32)
+    desc = Desc(family, n, m, 0, B, ld)
+    rc = _sens_lib().oracle_vjp_batch(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), _ptr(gx), _ptr(gy),
+                                      _ptr(gs), _ptr(dth), _ptr(st), int(nthreads))
+    if rc != 0:
+        raise ValueError(f"oracle_vjp_batch failed with code {rc}")
+    return dth, st
+
+
+def jvp_batch(family: int, n: int, m: int, theta, x, y, s, theta_dot, nthreads: int = 1):
+    """Oracle of mcpx_jvp_batch: theta_dot (B, K, p) → (zdot (B, K, n+2m), status (B,))."""
+    theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+    B, ld = theta.shape
+    p = theta_dim(family, n, m)
+    td = np.ascontiguousarray(theta_dot, dtype=np.float64).reshape(B, -1, p)
+    K = td.shape[1]
+    x, y, s = _f64(x, (B, n)), _f64(y, (B, m)), _f64(s, (B, m))
+    zd = np.empty((B, K, n + 2 * m))
+    st = np.empty(B, np.int32)
+    desc = Desc(family, n, m, 0, B, ld)
+    rc = _sens_lib().oracle_jvp_batch(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), int(K), _ptr(td),
+                                      _ptr(zd), _ptr(st), int(nthreads))
+    if rc != 0:
+        raise ValueError(f"oracle_jvp_batch failed with code {rc}")
+    return zd, st

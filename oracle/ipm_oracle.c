@@ -515,3 +515,217 @@ int oracle_solve_batch(const mcpx_desc* d, const double* theta, const double* x0
   pthread_mutex_destroy(&j.mu);
   return j.err ? MCPX_EINVAL : 0;
 }
+
+/* ======================================================================
+ * Sensitivities (reference src/AutoDiff.jl) — see include/mcpx.h.
+ *
+ * ∂z/∂θ = −(∇F_z)⁻¹ ∇F_θ at the returned (x, y, s), ∇F_z WITHOUT tol·I
+ * (src/AutoDiff.jl:18-40; Appendix A.10 of SURVEY.md).  The reference solves
+ * with a column-pivoted QR of −∇F_z (LAPACK geqp3, :39); this restatement uses
+ * lu_solve() above on ∇F_z (JVP) or ∇F_zᵀ (VJP): equal for nonsingular ∇F_z up
+ * to rounding (tests/test_oracle.py cross-checks against a numpy pivoted-QR
+ * restatement, oracle/ipm_ref.py).  Exactly singular ⇒ status 1, NaN outputs.
+ * ====================================================================== */
+
+/* (∇F_θ θ̇)_i: row i of F's θ-derivative applied to the tangent d (QP:
+ * ∂G/∂θ·d = Ṁx − ϕ̇ − Ȧᵀy, ∂H/∂θ·d = Ȧx − ḃ; affine: Ṗx + Q̇y + ġ,
+ * Ṙx + Ṡy + ḣ; complementarity rows 0).  fma chains as family_row(). */
+static double dtheta_row(int family, int n, int m, const double* d, const double* z, int i) {
+  const double* x = z;
+  const double* y = z + n;
+  const size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
+  double acc = 0.0;
+  if (i < n) {
+    if (family == MCPX_FAMILY_QP) {
+      for (int j = 0; j < n; ++j) acc = fma(d[(size_t)j * n + i], x[j], acc);
+      for (int k = 0; k < m; ++k) acc = fma(-d[nn + (size_t)i * m + k], y[k], acc);
+      return acc - d[nn + nm + m + i];
+    }
+    for (int j = 0; j < n; ++j) acc = fma(d[(size_t)j * n + i], x[j], acc);
+    for (int k = 0; k < m; ++k) acc = fma(d[nn + (size_t)k * n + i], y[k], acc);
+    return acc + d[nn + 2 * nm + mm + i];
+  }
+  if (i < n + m) {
+    const int k = i - n;
+    if (family == MCPX_FAMILY_QP) {
+      for (int j = 0; j < n; ++j) acc = fma(d[nn + (size_t)j * m + k], x[j], acc);
+      return acc - d[nn + nm + k];
+    }
+    for (int j = 0; j < n; ++j) acc = fma(d[nn + nm + (size_t)j * m + k], x[j], acc);
+    for (int q = 0; q < m; ++q) acc = fma(d[nn + 2 * nm + (size_t)q * m + k], y[q], acc);
+    return acc + d[nn + 2 * nm + mm + n + k];
+  }
+  return 0.0;
+}
+
+typedef struct sens_ws {
+  double *J, *JT, *b, *dz, *z, *row;
+  int *rem, *step, *prow;
+} sens_ws;
+
+static int sens_ws_alloc(sens_ws* w, int N) {
+  const size_t NN = (size_t)(N > 0 ? N : 1);
+  w->J = (double*)malloc(sizeof(double) * NN * NN);
+  w->JT = (double*)malloc(sizeof(double) * NN * NN);
+  w->b = (double*)malloc(sizeof(double) * NN);
+  w->dz = (double*)malloc(sizeof(double) * NN);
+  w->z = (double*)malloc(sizeof(double) * NN);
+  w->row = (double*)malloc(sizeof(double) * NN);
+  w->rem = (int*)malloc(sizeof(int) * NN);
+  w->step = (int*)malloc(sizeof(int) * NN);
+  w->prow = (int*)malloc(sizeof(int) * NN);
+  return !(w->J && w->JT && w->b && w->dz && w->z && w->row && w->rem && w->step && w->prow);
+}
+
+static void sens_ws_free(sens_ws* w) {
+  free(w->J); free(w->JT); free(w->b); free(w->dz); free(w->z); free(w->row);
+  free(w->rem); free(w->step); free(w->prow);
+}
+
+/* ∇F_z (no tol·I) at z, N×N row-major, via family_row (src/mcp.jl:97-120). */
+static void jacobian_z(int family, int n, int m, const double* th, const double* z, double* J) {
+  const int N = n + 2 * m;
+  for (int i = 0; i < N; ++i) (void)family_row(family, n, m, th, z, 0.0, i, J + (size_t)i * N);
+}
+
+typedef struct sens_job {
+  int jvp;
+  const mcpx_desc* d;
+  const double *theta, *x, *y, *s, *gx, *gy, *gs, *tdot;
+  int K;
+  double* out;
+  int32_t* status;
+  int64_t next;
+  pthread_mutex_t mu;
+  int err;
+} sens_job;
+
+static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
+  const mcpx_desc* d = j->d;
+  const int n = d->n, m = d->m, N = n + 2 * m;
+  const double* th = j->theta + b * d->theta_ld;
+  const int64_t p = oracle_theta_dim(d->family, n, m);
+  for (int i = 0; i < n; ++i) w->z[i] = j->x[b * n + i];
+  for (int k = 0; k < m; ++k) {
+    w->z[n + k] = j->y[b * m + k];
+    w->z[n + m + k] = j->s[b * m + k];
+  }
+  const double nanv = __builtin_nan("");
+  int failed = 0;
+  if (!j->jvp) {
+    /* rrule pullback, src/AutoDiff.jl:59-76: ∇F_zᵀ λ = g, ∂θ = −∇F_θᵀ λ */
+    jacobian_z(d->family, n, m, th, w->z, w->J);
+    for (int r = 0; r < N; ++r)
+      for (int c = 0; c < N; ++c) w->JT[(size_t)r * N + c] = w->J[(size_t)c * N + r];
+    for (int i = 0; i < n; ++i) w->b[i] = j->gx ? j->gx[b * n + i] : 0.0;
+    for (int k = 0; k < m; ++k) {
+      w->b[n + k] = j->gy ? j->gy[b * m + k] : 0.0;
+      w->b[n + m + k] = j->gs ? j->gs[b * m + k] : 0.0;
+    }
+    failed = lu_solve(N, w->JT, w->b, w->dz, w->rem, w->step, w->prow);
+    if (failed)
+      for (int i = 0; i < N; ++i) w->dz[i] = nanv;
+    const double* lx = w->dz;      /* λ of the G rows */
+    const double* ly = w->dz + n;  /* λ of the H − s rows */
+    const double* x = w->z;
+    const double* y = w->z + n;
+    double* o = j->out + b * p;
+    const size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
+    if (d->family == MCPX_FAMILY_QP) {
+      for (int c = 0; c < n; ++c)
+        for (int r = 0; r < n; ++r) o[(size_t)c * n + r] = -(lx[r] * x[c]);               /* ∂M_rc */
+      for (int c = 0; c < n; ++c)
+        for (int k = 0; k < m; ++k) o[nn + (size_t)c * m + k] = fma(lx[c], y[k], -(ly[k] * x[c]));  /* ∂A_kc */
+      for (int k = 0; k < m; ++k) o[nn + nm + k] = ly[k];                                  /* ∂b_k */
+      for (int i = 0; i < n; ++i) o[nn + nm + m + i] = lx[i];                              /* ∂ϕ_i */
+    } else {
+      for (int c = 0; c < n; ++c)
+        for (int r = 0; r < n; ++r) o[(size_t)c * n + r] = -(lx[r] * x[c]);               /* ∂P */
+      for (int c = 0; c < m; ++c)
+        for (int r = 0; r < n; ++r) o[nn + (size_t)c * n + r] = -(lx[r] * y[c]);          /* ∂Q */
+      for (int c = 0; c < n; ++c)
+        for (int k = 0; k < m; ++k) o[nn + nm + (size_t)c * m + k] = -(ly[k] * x[c]);     /* ∂R */
+      for (int c = 0; c < m; ++c)
+        for (int k = 0; k < m; ++k) o[nn + 2 * nm + (size_t)c * m + k] = -(ly[k] * y[c]); /* ∂S */
+      for (int i = 0; i < n; ++i) o[nn + 2 * nm + mm + i] = -lx[i];                        /* ∂g */
+      for (int k = 0; k < m; ++k) o[nn + 2 * nm + mm + n + k] = -ly[k];                    /* ∂h */
+    }
+  } else {
+    /* ForwardDiff Dual method, src/AutoDiff.jl:94-100: ż = −(∇F_z)⁻¹ ∇F_θ θ̇ per partial */
+    for (int c = 0; c < j->K; ++c) {
+      const double* dd = j->tdot + (b * j->K + c) * p;
+      double* o = j->out + (b * j->K + c) * N;
+      jacobian_z(d->family, n, m, th, w->z, w->J);
+      for (int i = 0; i < N; ++i) w->b[i] = -dtheta_row(d->family, n, m, dd, w->z, i);
+      const int f = lu_solve(N, w->J, w->b, w->dz, w->rem, w->step, w->prow);
+      failed |= f;
+      for (int i = 0; i < N; ++i) o[i] = f ? nanv : w->dz[i];
+    }
+  }
+  if (j->status) j->status[b] = failed ? 1 : 0;
+}
+
+static void* sens_worker(void* arg) {
+  sens_job* j = (sens_job*)arg;
+  sens_ws w;
+  if (sens_ws_alloc(&w, j->d->n + 2 * j->d->m)) {
+    pthread_mutex_lock(&j->mu);
+    j->err = 1;
+    pthread_mutex_unlock(&j->mu);
+    sens_ws_free(&w);
+    return NULL;
+  }
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    const int64_t b = j->next++;
+    pthread_mutex_unlock(&j->mu);
+    if (b >= j->d->batch) break;
+    sens_one(j, &w, b);
+  }
+  sens_ws_free(&w);
+  return NULL;
+}
+
+static int sens_run(sens_job* j, int nthreads) {
+  const mcpx_desc* d = j->d;
+  const int64_t pd = oracle_theta_dim(d->family, d->n, d->m);
+  if (pd < 0 || d->n + d->m < 1 || d->batch < 0 || d->theta_ld < pd || !j->theta || !j->out) return MCPX_EINVAL;
+  if (d->n + 2 * d->m > MCPX_MAX_KKT_DIM) return MCPX_EUNSUPPORTED;
+  j->next = 0;
+  j->err = 0;
+  pthread_mutex_init(&j->mu, NULL);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads == 1) {
+    sens_worker(j);
+  } else {
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * nthreads);
+    for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, sens_worker, j);
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    free(th);
+  }
+  pthread_mutex_destroy(&j->mu);
+  return j->err ? MCPX_EINVAL : 0;
+}
+
+/* Same argument meaning as mcpx_vjp_batch / mcpx_jvp_batch (host buffers). */
+int oracle_vjp_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                     const double* s, const double* gx, const double* gy, const double* gs,
+                     double* dtheta, int32_t* status, int nthreads) {
+  if (!d) return MCPX_EINVAL;
+  sens_job j;
+  memset(&j, 0, sizeof j);
+  j.jvp = 0; j.d = d; j.theta = theta; j.x = x; j.y = y; j.s = s;
+  j.gx = gx; j.gy = gy; j.gs = gs; j.out = dtheta; j.status = status;
+  return sens_run(&j, nthreads);
+}
+
+int oracle_jvp_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                     const double* s, int32_t n_partials, const double* theta_dot, double* zdot,
+                     int32_t* status, int nthreads) {
+  if (!d || n_partials < 0 || (n_partials > 0 && !theta_dot)) return MCPX_EINVAL;
+  sens_job j;
+  memset(&j, 0, sizeof j);
+  j.jvp = 1; j.d = d; j.theta = theta; j.x = x; j.y = y; j.s = s;
+  j.tdot = theta_dot; j.K = n_partials; j.out = zdot; j.status = status;
+  return sens_run(&j, nthreads);
+}

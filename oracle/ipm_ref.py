@@ -145,3 +145,45 @@ def solve(family, theta, n, m, *, x0=None, y0=None, s0=None, tol=1e-4, max_inner
     if outer_iters == max_outer_iters:
         status = "failed"
     return Solution(status, x, y, s, kkt_error, eps, outer_iters, newton, trace)
+
+
+# ---------------------------------------------------------------------------
+# sensitivities (src/AutoDiff.jl)
+
+
+def jacobian_theta(family, theta, n, m, x, y, s):
+    """∇F_θ (N × p) at (x, y, s).  F is affine in θ for both families, so column t
+    is F(z; e_t) − F(z; 0) (with the θ-free terms cancelling exactly)."""
+    p = theta_dim(family, n, m)
+    z0 = F_and_jacobian(unpack(family, np.zeros(p), n, m), x, y, s, 0.0)[0]
+    cols = np.empty((n + 2 * m, p))
+    for t in range(p):
+        e = np.zeros(p)
+        e[t] = 1.0
+        cols[:, t] = F_and_jacobian(unpack(family, e, n, m), x, y, s, 0.0)[0] - z0
+    return cols
+
+
+def dz_dtheta(family, theta, n, m, x, y, s):
+    """src/AutoDiff.jl:18-40: `qr(−∇F_z, ColumnNorm()) \\ ∇F_θ` (LAPACK geqp3, as
+    the reference), evaluated at the solution WITHOUT tol·I.  For a full-rank
+    ∇F_z the pivoted-QR solve is P R⁻¹ Qᵀ B."""
+    _, J = F_and_jacobian(unpack(family, theta, n, m), x, y, s, 0.0)
+    B = jacobian_theta(family, theta, n, m, x, y, s)
+    Q, R, piv = scipy.linalg.qr(-J, pivoting=True)
+    sol = scipy.linalg.solve_triangular(R, Q.T @ B)
+    out = np.empty_like(sol)
+    out[piv] = sol
+    return out
+
+
+def vjp(family, theta, n, m, x, y, s, gx, gy, gs):
+    """rrule pullback, src/AutoDiff.jl:59-76: ∂z∂θ[x rows]ᵀ ∂l∂x + ∂z∂θ[y rows]ᵀ ∂l∂y + ∂z∂θ[s rows]ᵀ ∂l∂s."""
+    D = dz_dtheta(family, theta, n, m, x, y, s)
+    return D[:n].T @ gx + D[n : n + m].T @ gy + D[n + m :].T @ gs
+
+
+def jvp(family, theta, n, m, x, y, s, theta_dot):
+    """ForwardDiff Dual method, src/AutoDiff.jl:94-100: z_p = ∂z∂θ · θ_p; theta_dot (K, p) → (K, N)."""
+    D = dz_dtheta(family, theta, n, m, x, y, s)
+    return (D @ np.atleast_2d(theta_dot).T).T

@@ -1,0 +1,271 @@
+"""Sensitivities of the solution w.r.t. θ (reference src/AutoDiff.jl).
+
+CPU (oracle, test infrastructure):
+  * the C oracle's pullback / tangents against the committed fixtures
+    (tests/golden/sens_*.npz, bit-exact);
+  * against the independent pivoted-QR restatement of `_solve_jacobian_θ`
+    (oracle/ipm_ref.py, LAPACK geqp3 like the reference, src/AutoDiff.jl:39)
+    within 1e-8 relative on well-conditioned solved instances;
+  * the reference's own AD test (test/runtests.jl:65-85): reverse-mode gradient
+    of f(θ) = Σx² + Σy² on the README QP against finite differences and against
+    forward mode, atol 1e-3 as the reference.
+GPU (MI355X, through the C ABI): bit-exact against the oracle on the fixtures,
+random QP / affine batches (incl. failed solves, K > MCPX_JVP_RHS partials,
+NULL cotangent blocks, exactly singular ∇F_z), device vs host API, and the
+size-independent adjoint identity ⟨g, ż⟩ = ⟨∂θ, θ̇⟩ at the C5 size.
+"""
+
+from __future__ import annotations
+
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from mcp_amd import _abi
+from mcp_amd.qp_benchmark import generate_random_parameter
+from oracle import ipm_ref
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "sens_*.npz")))
+
+
+def _same(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+
+
+def random_affine_theta(rng, n, m, B):
+    """Monotone affine MCPs G = P x + Q y + g, H = R x + S y + h with P ≻ 0,
+    Q = −Rᵀ and S ⪰ 0 diagonal (the shape of a game's KKT system, src/game.jl)."""
+    out = []
+    for _ in range(B):
+        L = rng.standard_normal((n, n))
+        P = L @ L.T / n + np.eye(n)
+        R = rng.standard_normal((m, n))
+        S = np.diag(rng.uniform(0.0, 0.5, m))
+        g, h = rng.standard_normal(n), rng.standard_normal(m)
+        out.append(np.concatenate([P.flatten("F"), (-R.T).flatten("F"), R.flatten("F"), S.flatten("F"), g, h]))
+    return np.array(out)
+
+
+# ---------------------------------------------------------------------------
+# CPU: oracle
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=lambda p: os.path.basename(p)[5:-4])
+def test_oracle_sensitivities_reproduce_fixtures(oracle_lib, path):
+    d = np.load(path, allow_pickle=False)
+    fam, n, m = int(d["family"]), int(d["n"]), int(d["m"])
+    dth, st = oracle_lib.vjp_batch(fam, n, m, d["theta"], d["x"], d["y"], d["s"], d["gx"], d["gy"], d["gs"])
+    assert _same(dth, d["dtheta"]) and _same(st, d["vjp_status"])
+    zd, stj = oracle_lib.jvp_batch(fam, n, m, d["theta"], d["x"], d["y"], d["s"], d["theta_dot"])
+    assert _same(zd, d["zdot"]) and _same(stj, d["jvp_status"])
+
+
+CASES = [(0, 2, 2), (0, 16, 8), (0, 32, 16), (0, 5, 0), (0, 3, 7), (1, 6, 4), (1, 12, 10)]
+
+
+@pytest.mark.parametrize("fam,n,m", CASES)
+def test_oracle_matches_pivoted_qr_restatement(oracle_lib, fam, n, m):
+    """1e-8 relative (north_star's iterate bar) wherever ∇F_z is well conditioned."""
+    rng = np.random.default_rng(100 + n + m)
+    B = 4
+    th = generate_random_parameter(rng, n, m, 0.0, batch=B) if fam == 0 else random_affine_theta(rng, n, m, B)
+    r = oracle_lib.solve_batch(fam, n, m, th, tol=1e-6)
+    gx, gy, gs = rng.standard_normal((B, n)), rng.standard_normal((B, m)), rng.standard_normal((B, m))
+    td = rng.standard_normal((B, 3, th.shape[1]))
+    dth, st = oracle_lib.vjp_batch(fam, n, m, th, r["x"], r["y"], r["s"], gx, gy, gs)
+    zd, stj = oracle_lib.jvp_batch(fam, n, m, th, r["x"], r["y"], r["s"], td)
+    checked = 0
+    for b in range(B):
+        _, J = ipm_ref.F_and_jacobian(ipm_ref.unpack(fam, th[b], n, m), r["x"][b], r["y"][b], r["s"][b], 0.0)
+        if r["status"][b] != 0 or np.linalg.cond(J) > 1e8:
+            continue
+        assert st[b] == 0 and stj[b] == 0
+        ref = ipm_ref.vjp(fam, th[b], n, m, r["x"][b], r["y"][b], r["s"][b], gx[b], gy[b], gs[b])
+        assert np.abs(ref - dth[b]).max() <= 1e-8 * max(1.0, np.abs(ref).max())
+        refj = ipm_ref.jvp(fam, th[b], n, m, r["x"][b], r["y"][b], r["s"][b], td[b])
+        assert np.abs(refj - zd[b]).max() <= 1e-8 * max(1.0, np.abs(refj).max())
+        checked += 1
+    assert checked >= 2
+
+
+def test_oracle_singular_jacobian_is_status_not_error(oracle_lib):
+    """s_k = y_k = 0 zeroes a complementarity row of ∇F_z: status 1, NaN outputs
+    (the reference's pivoted QR would return a basic least-squares solution)."""
+    th = generate_random_parameter(np.random.default_rng(5), 4, 2, 0.0, batch=1)
+    x, y, s = np.ones((1, 4)), np.array([[0.0, 1.0]]), np.array([[0.0, 1.0]])
+    dth, st = oracle_lib.vjp_batch(0, 4, 2, th, x, y, s, np.ones((1, 4)))
+    assert st[0] == 1 and np.isnan(dth).all()
+    zd, stj = oracle_lib.jvp_batch(0, 4, 2, th, x, y, s, np.ones((1, 2, th.shape[1])))
+    assert stj[0] == 1 and np.isnan(zd).all()
+
+
+def test_reference_ad_test_restated(oracle_lib):
+    """test/runtests.jl:65-85 on the README QP through the oracle: ∇f by the
+    pullback (Zygote rrule) vs FiniteDiff central differences and vs forward mode,
+    atol 1e-3.  f(θ) = Σx² + Σy², θ = ϕ ∈ ℝ² (README.md:51-57)."""
+    from tests.golden.make_golden import readme_qp_theta
+
+    theta = np.array([-0.5, 0.5])
+
+    def f(t):
+        r = oracle_lib.solve_batch(0, 2, 2, readme_qp_theta(t)[None, :])
+        return float((r["x"] ** 2).sum() + (r["y"] ** 2).sum()), r
+
+    _, r = f(theta)
+    th = readme_qp_theta(theta)[None, :]
+    dth, st = oracle_lib.vjp_batch(0, 2, 2, th, r["x"], r["y"], r["s"], 2 * r["x"], 2 * r["y"], np.zeros((1, 2)))
+    assert st[0] == 0
+    grad_rev = dth[0, -2:]  # θ = ϕ occupies the last n entries of the QP layout
+    h = 1e-6
+    grad_fd = np.array([(f(theta + h * e)[0] - f(theta - h * e)[0]) / (2 * h) for e in np.eye(2)])
+    np.testing.assert_allclose(grad_rev, grad_fd, atol=1e-3)
+    td = np.zeros((1, 2, th.shape[1]))
+    td[0, 0, -2], td[0, 1, -1] = 1.0, 1.0
+    zd, _ = oracle_lib.jvp_batch(0, 2, 2, th, r["x"], r["y"], r["s"], td)
+    grad_fwd = np.array([2 * r["x"][0] @ zd[0, c, :2] + 2 * r["y"][0] @ zd[0, c, 2:4] for c in range(2)])
+    np.testing.assert_allclose(grad_rev, grad_fwd, atol=1e-3)
+
+
+def test_abi_sensitivity_argument_errors():
+    import ctypes as C
+
+    from mcp_amd._lib import lib
+
+    L = lib()
+    big = _abi.Desc(0, 40, 16, 0, 1, _abi.theta_dim(0, 40, 16))  # n + 2m = 72 > 64
+    buf = np.zeros(8192)
+    ptr = buf.ctypes.data
+    assert L.mcpx_vjp_batch(C.byref(big), ptr, ptr, ptr, ptr, None, None, None, 1, ptr, None) == \
+        _abi.MCPX_EUNSUPPORTED
+    bad = _abi.Desc(0, 2, 2, 0, 1, 3)  # theta_ld < p
+    assert L.mcpx_vjp_batch(C.byref(bad), ptr, ptr, ptr, ptr, None, None, None, 1, ptr, None) == _abi.MCPX_EINVAL
+    ok = _abi.Desc(0, 2, 2, 0, 1, _abi.theta_dim(0, 2, 2))
+    assert L.mcpx_jvp_batch(C.byref(ok), ptr, ptr, ptr, ptr, -1, ptr, 1, ptr, None) == _abi.MCPX_EINVAL
+    assert L.mcpx_vjp_batch(C.byref(ok), ptr, None, ptr, ptr, None, None, None, 1, ptr, None) == _abi.MCPX_EINVAL
+    if L.mcpx_device_count() == 0:  # no CPU fallback
+        assert L.mcpx_vjp_batch(C.byref(ok), ptr, ptr, ptr, ptr, None, None, None, 1, ptr, None) == \
+            _abi.MCPX_ENODEV
+        assert L.mcpx_jvp_batch(C.byref(ok), ptr, ptr, ptr, ptr, 1, ptr, 1, ptr, None) == _abi.MCPX_ENODEV
+
+
+# ---------------------------------------------------------------------------
+# GPU: HIP kernels against the oracle, bit-exact
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", FIXTURES, ids=lambda p: os.path.basename(p)[5:-4])
+def test_gpu_sensitivities_fixtures(gpu, path):
+    from mcp_amd.batch import jvp_batch, vjp_batch
+
+    d = np.load(path, allow_pickle=False)
+    fam, n, m = int(d["family"]), int(d["n"]), int(d["m"])
+    dth, st = vjp_batch(fam, n, m, d["theta"], d["x"], d["y"], d["s"], d["gx"], d["gy"], d["gs"])
+    assert _same(st, d["vjp_status"]) and _same(dth, d["dtheta"])
+    zd, stj = jvp_batch(fam, n, m, d["theta"], d["x"], d["y"], d["s"], d["theta_dot"])
+    assert _same(stj, d["jvp_status"]) and _same(zd, d["zdot"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fam,n,m,sp", [(0, 2, 2, 0.0), (0, 16, 8, 0.0), (0, 16, 8, 0.9), (0, 32, 16, 0.0),
+                                        (0, 5, 0, 0.0), (0, 3, 7, 0.0), (0, 7, 20, 0.0), (0, 1, 1, 0.0),
+                                        (1, 6, 4, 0.0), (1, 12, 10, 0.0), (1, 20, 22, 0.0)])
+@pytest.mark.parametrize("K", [1, 8, 13])
+def test_gpu_sensitivities_match_oracle(gpu, oracle_lib, fam, n, m, sp, K):
+    from mcp_amd.batch import jvp_batch, vjp_batch
+
+    rng = np.random.default_rng(7 * n + m + K)
+    B = 64
+    th = generate_random_parameter(rng, n, m, sp, batch=B) if fam == 0 else random_affine_theta(rng, n, m, B)
+    r = oracle_lib.solve_batch(fam, n, m, th, tol=1e-6)
+    gx, gy, gs = rng.standard_normal((B, n)), rng.standard_normal((B, m)), rng.standard_normal((B, m))
+    dth, st = vjp_batch(fam, n, m, th, r["x"], r["y"], r["s"], gx, gy, gs)
+    rdth, rst = oracle_lib.vjp_batch(fam, n, m, th, r["x"], r["y"], r["s"], gx, gy, gs)
+    np.testing.assert_array_equal(st, rst)
+    assert _same(dth, rdth)
+    td = rng.standard_normal((B, K, th.shape[1]))
+    zd, stj = jvp_batch(fam, n, m, th, r["x"], r["y"], r["s"], td)
+    rzd, rstj = oracle_lib.jvp_batch(fam, n, m, th, r["x"], r["y"], r["s"], td)
+    np.testing.assert_array_equal(stj, rstj)
+    assert _same(zd, rzd)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["gx", "gy", "gs"])
+def test_gpu_vjp_null_cotangent_blocks(gpu, oracle_lib, which):
+    """A NULL block is ChainRulesCore's ZeroTangent for that field."""
+    from mcp_amd.batch import vjp_batch
+
+    rng = np.random.default_rng(3)
+    n, m, B = 16, 8, 32
+    th = generate_random_parameter(rng, n, m, 0.0, batch=B)
+    r = oracle_lib.solve_batch(0, n, m, th, tol=1e-6)
+    g = dict(gx=rng.standard_normal((B, n)), gy=rng.standard_normal((B, m)), gs=rng.standard_normal((B, m)))
+    g[which] = None
+    dth, st = vjp_batch(0, n, m, th, r["x"], r["y"], r["s"], **g)
+    rdth, _ = oracle_lib.vjp_batch(0, n, m, th, r["x"], r["y"], r["s"], **g)
+    assert _same(dth, rdth)
+
+
+@pytest.mark.gpu
+def test_gpu_singular_jacobian(gpu, oracle_lib):
+    from mcp_amd.batch import jvp_batch, vjp_batch
+
+    th = generate_random_parameter(np.random.default_rng(5), 4, 2, 0.0, batch=2)
+    x, y, s = np.ones((2, 4)), np.array([[0.0, 1.0], [1.0, 2.0]]), np.array([[0.0, 1.0], [0.5, 0.25]])
+    dth, st = vjp_batch(0, 4, 2, th, x, y, s, np.ones((2, 4)))
+    assert st.tolist() == [1, 0] and np.isnan(dth[0]).all() and np.isfinite(dth[1]).all()
+    zd, stj = jvp_batch(0, 4, 2, th, x, y, s, np.ones((2, 3, th.shape[1])))
+    assert stj.tolist() == [1, 0] and np.isnan(zd[0]).all()
+    rdth, _ = oracle_lib.vjp_batch(0, 4, 2, th, x, y, s, np.ones((2, 4)))
+    assert _same(dth, rdth)
+
+
+@pytest.mark.gpu
+def test_gpu_device_api_matches_host_api(gpu, oracle_lib):
+    import torch
+
+    from mcp_amd.batch import jvp_batch_device, vjp_batch, vjp_batch_device
+
+    rng = np.random.default_rng(9)
+    n, m, B = 32, 16, 256
+    th = generate_random_parameter(rng, n, m, 0.0, batch=B)
+    r = oracle_lib.solve_batch(0, n, m, th, tol=1e-6)
+    gx = rng.standard_normal((B, n))
+    dev = torch.device("cuda", 0)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    dth_d, st_d = vjp_batch_device(0, n, m, T(th), T(r["x"]), T(r["y"]), T(r["s"]), gx=T(gx))
+    torch.cuda.synchronize()
+    dth_h, st_h = vjp_batch(0, n, m, th, r["x"], r["y"], r["s"], gx)
+    assert _same(dth_d.cpu().numpy(), dth_h) and _same(st_d.cpu().numpy(), st_h)
+    td = rng.standard_normal((B, 2, th.shape[1]))
+    zd_d, _ = jvp_batch_device(0, n, m, T(th), T(r["x"]), T(r["y"]), T(r["s"]), T(td))
+    torch.cuda.synchronize()
+    rzd, _ = oracle_lib.jvp_batch(0, n, m, th, r["x"], r["y"], r["s"], td)
+    assert _same(zd_d.cpu().numpy(), rzd)
+
+
+@pytest.mark.gpu
+def test_gpu_c5_adjoint_identity(gpu):
+    """BASELINE C5 size (C3 QPs, batch 4096): solve on the GPU, then the
+    size-independent duality of the two sensitivity kernels,
+    ⟨g, (∂z/∂θ) θ̇⟩ = ⟨(∂z/∂θ)ᵀ g, θ̇⟩ per instance (1e-9 relative)."""
+    from mcp_amd.batch import jvp_batch, solve_batch, vjp_batch
+
+    rng = np.random.default_rng(2024)
+    n, m, B = 32, 16, 4096
+    th = generate_random_parameter(rng, n, m, 0.0, batch=B)
+    r = solve_batch(0, n, m, th, tol=1e-6, linear_solver="schur")
+    assert (r["status"] == 0).all()
+    g = rng.standard_normal((B, n + 2 * m))
+    td = rng.standard_normal((B, 1, th.shape[1]))
+    dth, st = vjp_batch(0, n, m, th, r["x"], r["y"], r["s"], g[:, :n], g[:, n:n + m], g[:, n + m:])
+    zd, stj = jvp_batch(0, n, m, th, r["x"], r["y"], r["s"], td)
+    assert (st == 0).all() and (stj == 0).all()
+    lhs = np.einsum("bi,bi->b", g, zd[:, 0])
+    rhs = np.einsum("bp,bp->b", dth, td[:, 0])
+    scale = np.abs(g).max(1) * np.abs(zd[:, 0]).max(1) * (n + 2 * m)
+    assert (np.abs(lhs - rhs) <= 1e-9 * np.maximum(scale, 1.0)).all()
