@@ -8,4 +8,4 @@ on top of hand-written gfx950 HIP kernels behind the C ABI of include/mcpx.h.
 from . import _abi  # noqa: F401
 from ._lib import MCPXError  # noqa: F401
 
-__version__ = "1.0.0"
+__version__ = "1.1.0"

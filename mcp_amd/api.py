@@ -242,6 +242,22 @@ class ThetaMap:
             res += self.vjp_nonlin(np.atleast_2d(theta), g)
         return res
 
+    def jvp(self, theta, t_in):
+        """(∂θ'/∂θ) θ̇ per instance and tangent: (B, K, p) → (B, K, p') (host numpy),
+        the forward-mode counterpart of `vjp` (src/AutoDiff.jl:84-100)."""
+        td = np.asarray(t_in, np.float64)
+        B, K = td.shape[0], td.shape[1]
+        out = np.zeros((B, K, self.p_out))
+        if len(self.dst):
+            np.add.at(np.moveaxis(out, 2, 0), self.dst, np.moveaxis(td[:, :, self.src] * self.coef, 2, 0))
+        if self._nonlin_grad:
+            th = np.atleast_2d(np.asarray(theta, np.float64))
+            cols = [th[:, k] for k in range(self.p_in)]
+            for i, grads in self._nonlin_grad:
+                for k, f in grads:
+                    out[:, :, i] += np.broadcast_to(f(*cols), (B,))[:, None] * td[:, :, k]
+        return out
+
     def vjp_nonlin(self, theta, g):
         B = g.shape[0]
         res = np.zeros((B, self.p_in))

@@ -9,6 +9,10 @@
 
 namespace mcpx {
 
+// Internal per-instance status of the two-pass SCHUR launch (ipm_solve_kernel
+// PASS 1 → 2); never returned: the second pass overwrites it with 0 / 1.
+constexpr int32_t STATUS_DEFERRED = 2;
+
 struct KernelArgs {
   const double* theta;
   int64_t theta_ld;

@@ -398,93 +398,6 @@ __device__ __forceinline__ void qp_residuals(const double* __restrict__ th, cons
   }
 }
 
-// Lane ln's row of the Schur complement from its LDS tile (zero outside n×n).
-template <int NMAX>
-__device__ __forceinline__ void load_schur_rows(const double* sS, int ln, int n, double (&a)[NMAX]) {
-#pragma unroll
-  for (int j = 0; j < NMAX; ++j) a[j] = (ln < n && j < n) ? sS[min(ln, NMAX - 1) * (NMAX + 1) + j] : 0.0;
-}
-
-// SCHUR path, part 2: the n×n Schur complement S = (M + tol·I) + Aᵀ D⁻¹ A on the
-// fp64 matrix cores.  v_mfma_f64_16x16x4_f64 is an ordered fma chain over its
-// 4 k's (tools/ubench_mfma64.hip), so K-chunked accumulation reproduces the
-// oracle's sequential fma chain bit for bit (k ≥ m are zero operands).
-// Operands come straight from θ in fragment layout: A-fragment lane l holds
-// A_ki with i = 16I + (l & 15), k = 4c + (l >> 4) (contiguous in k); the
-// B-fragment holds A_kj / D_k with j = 16J + (l & 15).  The tiles land in LDS
-// (row-major, stride NMAX+1) and each x-lane reads back its row.
-template <int NMAX>
-__device__ __forceinline__ void qp_schur_form(const double* __restrict__ th, const double* sD, double* sS, int ln,
-                                              int n, int m, double tol) {
-  constexpr int NT = (NMAX + 15) / 16;
-  const int nn = n * n;
-  const int lr = ln >> 4, lc = ln & 15;
-  d4 acc[NT][NT];
-  {  // C = M + tol·I, all NT·NT·4 loads issued before any use
-    double mv[NT][NT][4];
-#pragma unroll
-    for (int I = 0; I < NT; ++I)
-#pragma unroll
-      for (int J = 0; J < NT; ++J)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = min(16 * I + lr + 4 * r, n - 1), col = min(16 * J + lc, n - 1);
-          mv[I][J][r] = th[col * n + row];
-        }
-#pragma unroll
-    for (int I = 0; I < NT; ++I)
-#pragma unroll
-      for (int J = 0; J < NT; ++J)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * I + lr + 4 * r, col = 16 * J + lc;
-          const bool in = row < n && col < n;
-          const double v = mv[I][J][r];
-          acc[I][J][r] = in ? (row == col ? v + tol : v) : 0.0;  // M_ij (+ tol on the diagonal)
-        }
-  }
-  const int kc = (m + 3) / 4;
-  // K-chunk c: lane l's A_ki for i = 16I + lc, k = 4c + lr; loads of chunk c+1
-  // are issued before the MFMAs of chunk c (software pipelining)
-  double nxt[NT];
-#pragma unroll
-  for (int I = 0; I < NT; ++I) nxt[I] = th[nn + min(16 * I + lc, n - 1) * m + min(lr, max(m - 1, 0))];
-  for (int c = 0; c < kc; ++c) {
-    const int k = 4 * c + lr;
-    const bool kin = k < m;
-    const double dk = sD[kin ? k : 0];
-    double cur[NT];
-#pragma unroll
-    for (int I = 0; I < NT; ++I) cur[I] = nxt[I];
-    if (c + 1 < kc) {
-      const int k1 = min(k + 4, m - 1);
-#pragma unroll
-      for (int I = 0; I < NT; ++I) nxt[I] = th[nn + min(16 * I + lc, n - 1) * m + k1];
-    }
-    double af[NT], bf[NT];
-#pragma unroll
-    for (int I = 0; I < NT; ++I) {
-      const bool in = kin && 16 * I + lc < n;
-      af[I] = in ? cur[I] : 0.0;        // A_ki
-      bf[I] = in ? cur[I] / dk : 0.0;   // A_kj / D_k  (j = 16J + lc: the same index pattern)
-    }
-#pragma unroll
-    for (int I = 0; I < NT; ++I)
-#pragma unroll
-      for (int J = 0; J < NT; ++J) acc[I][J] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[I], bf[J], acc[I][J], 0, 0, 0);
-  }
-#pragma unroll
-  for (int I = 0; I < NT; ++I)
-#pragma unroll
-    for (int J = 0; J < NT; ++J)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * I + lr + 4 * r, col = 16 * J + lc;
-        if (row < n && col < n) sS[row * (NMAX + 1) + col] = acc[I][J][r];
-      }
-  __syncthreads();
-}
-
 // ---- 2-D Gauss-Jordan on the matrix-core output layout (SCHUR, SPD) --------
 //
 // The Schur complement is formed transposed on the matrix cores (the A fragment
@@ -777,16 +690,56 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
 
 }  // namespace
 
+// v of lane `src` (ds_bpermute through the LDS crossbar; no LDS allocation).
+__device__ __forceinline__ double bperm_f64(double v, int src) {
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+// Row `ln` of S (lane-per-row layout of the pivoting LU) from the 2-D matrix-core
+// layout of qp_schur_form_2d: S[i][j] sits in tile (j >> 4, i >> 4), element
+// (j >> 2) & 3 of lane 16·(j & 3) + (i & 15).  Entries outside n×n are 0.
+template <int NT, int NMAX>
+__device__ __forceinline__ void schur_rows_from_2d(const d4 (&acc)[NT][NT], int ln, int n, double (&a)[NMAX]) {
+  const int half = ln >> 4, lc = ln & 15;
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) {
+    const int I = j >> 4, r = (j >> 2) & 3, src = 16 * (j & 3) + lc;
+    double v = 0.0;
+#pragma unroll
+    for (int J = 0; J < NT; ++J) {
+      const double t = bperm_f64(acc[I][J][r], src);
+      if (half == J) v = t;
+    }
+    a[j] = (ln < n && j < n) ? v : 0.0;
+  }
+}
+
 // NC, MC > 0: compile-time (n, m) specialisation; 0: runtime n, m.
 // SOLVER: MCPX_LINSOLVE_REDUCED (slack-eliminated (n+m)-dim system), _DENSE
 // (full (n+2m)-dim system) or _SCHUR (QP family, n×n Schur complement on MFMA).
-template <int NMAX, int FAMILY, int NC, int MC, int SOLVER>
-__global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
+//
+// PASS (SCHUR only; 0 otherwise) splits the solve over two launches so that the
+// common path is compiled without the pivoting-LU fallback, whose row-per-lane
+// S adds ~22 VGPRs to the whole kernel (94 → 116 at C3: 5 → 4 waves/SIMD):
+//   1  fast pass: SPD Gauss-Jordan only.  An instance whose M is not symmetric,
+//      or whose S stops being numerically SPD at some Newton step, is abandoned
+//      with status = STATUS_DEFERRED;
+//   2  second pass over the same grid: the instances marked deferred are solved
+//      again from the start with every path compiled in (the computation is
+//      deterministic, so they end bit-identical to a single complete pass); all
+//      others exit at once.
+template <int NMAX, int FAMILY, int NC, int MC, int SOLVER, int PASS>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 5 : 1, 8))) void ipm_solve_kernel(const KernelArgs args) {
   constexpr bool RED = SOLVER != MCPX_LINSOLVE_DENSE;  // lanes [0,n) x, [n,n+m) (y, s)
   constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR;
+  static_assert(SCH || PASS == 0, "two-pass launch is for the SCHUR solver only");
+  if constexpr (PASS == 2) {
+    if (__builtin_amdgcn_readfirstlane(args.status[blockIdx.x]) != STATUS_DEFERRED) return;
+  }
   __shared__ double zs[64];
   __shared__ double sD[SCH ? 64 : 1], sT[SCH ? 64 : 1];
-  __shared__ double sS[SCH ? NMAX * (NMAX + 1) : 1];
   __shared__ double sB[SCH ? 64 : 1];  // rr, restored for the LU fallback
   const int lane = threadIdx.x;
   const int64_t inst = blockIdx.x;
@@ -827,6 +780,12 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
       for (int b = 0; b < 8; ++b) asym |= (lane < n && j0 + b < n) && !(c[b] == t[b]);
     }
     spd_try = ballot(asym) == 0ull;
+    if constexpr (PASS == 1) {
+      if (!spd_try) {  // needs the pivoting LU at every step: second pass
+        if (lane == 0) args.status[inst] = STATUS_DEFERRED;
+        return;
+      }
+    }
   }
 
   double eps = 1.0;                    // :67
@@ -907,10 +866,18 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
           for (int J = 0; J < NT; ++J)
             if ((ln >> 4) == J) dz = x2[J];  // lane 16J + lc owns row 16J + lc
         }
-        if (!ok) {  // M not symmetric, or S not numerically SPD: pivoting LU on the same S
-          __syncthreads();
-          qp_schur_form<NMAX>(th, sD, sS, ln, n, m, tol);
-          load_schur_rows<NMAX>(sS, ln, n, a);
+        if constexpr (PASS == 1) {
+          if (!ok) {  // S not numerically SPD at this step: second pass
+            if (lane == 0) args.status[inst] = STATUS_DEFERRED;
+            return;
+          }
+        } else if (!ok) {  // M not symmetric, or S not numerically SPD: pivoting LU on the same S
+          // S again in the matrix-core layout, rows gathered across lanes with
+          // ds_bpermute: no n×n LDS tile, so LDS (2 KB per wave) does not cap occupancy
+          constexpr int NT = (NMAX + 15) / 16;
+          d4 acc4[NT][NT];
+          qp_schur_form_2d<NT>(th, sD, ln, n, m, tol, acc4);
+          schur_rows_from_2d<NT, NMAX>(acc4, ln, n, a);
           rhs = sB[ln];
           ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
         }
@@ -1024,8 +991,15 @@ __global__ __launch_bounds__(64) void ipm_solve_kernel(const KernelArgs args) {
 // Launch helper used by the instantiation units.
 template <int NMAX, int FAMILY, int NC, int MC, int SOLVER>
 hipError_t launch_one(const KernelArgs& args, int64_t batch, hipStream_t stream) {
-  hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER>), dim3((unsigned)batch), dim3(64), 0, stream,
-                     args);
+  if constexpr (SOLVER == MCPX_LINSOLVE_SCHUR) {  // fast pass, then the deferred instances
+    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 1>), dim3((unsigned)batch), dim3(64), 0,
+                       stream, args);
+    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 2>), dim3((unsigned)batch), dim3(64), 0,
+                       stream, args);
+  } else {
+    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 0>), dim3((unsigned)batch), dim3(64), 0,
+                       stream, args);
+  }
   return hipGetLastError();
 }
 

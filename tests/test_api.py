@@ -290,3 +290,84 @@ def test_device_theta(gpu):
     host = solve(InteriorPoint(), mcp, th.cpu().numpy())
     np.testing.assert_array_equal(sol.x.cpu().numpy(), host.x)
     assert sol.status.cpu().tolist() == [0, 0]
+
+
+# ---------------------------------------------------------------- AutoDiff mirror (src/AutoDiff.jl)
+
+
+def test_theta_map_jvp_is_the_adjoint_of_vjp():
+    t = make_variables("θ", 3)
+    tm = ThetaMap([t[0], -t[1], 2 * t[0] + t[2] - 1.5, 4.0, t[1] * t[2]], list(t))
+    rng = np.random.default_rng(4)
+    th, td, g = rng.standard_normal((5, 3)), rng.standard_normal((5, 2, 3)), rng.standard_normal((5, 5))
+    np.testing.assert_allclose(np.einsum("bkp,bp->bk", tm.jvp(th, td), g),
+                               np.einsum("bkq,bq->bk", td, tm.vjp(th, g)), rtol=1e-12)
+
+
+def test_missing_sensitivities_is_an_argument_error():
+    """src/AutoDiff.jl:19-23."""
+    from mcp_amd.autodiff import rrule
+
+    mcp = PrimalDualMCP(G, H, unconstrained_dimension=2, constrained_dimension=2, parameter_dimension=2,
+                        compute_sensitivities=False)
+    with pytest.raises(ValueError, match="compute_sensitivities"):
+        rrule(solve, InteriorPoint(), mcp, θ)
+
+
+def _readme_f(sol):
+    return float(np.sum(sol.x ** 2) + np.sum(sol.y ** 2))
+
+
+@pytest.mark.gpu
+def test_autodiff_reference_test(gpu):
+    """test/runtests.jl:65-85: reverse (rrule) vs forward (Dual) vs finite differences, atol 1e-3."""
+    from mcp_amd.autodiff import NoTangent, rrule, solve_dual
+
+    mcp = basic_mcp()
+    sol, pullback = rrule(solve, InteriorPoint(), mcp, θ)
+    grads = pullback({"x": 2 * sol.x, "y": 2 * sol.y})
+    assert grads[:3] == (NoTangent(), NoTangent(), NoTangent())
+    g_rev = grads[3]
+    h = 1e-6
+    g_fd = np.array([(_readme_f(solve(InteriorPoint(), mcp, θ + h * e)) -
+                      _readme_f(solve(InteriorPoint(), mcp, θ - h * e))) / (2 * h) for e in np.eye(2)])
+    np.testing.assert_allclose(g_rev, g_fd, atol=1e-3)
+    d = solve_dual(InteriorPoint(), mcp, θ, np.eye(2))  # partials: the identity seeds
+    g_fwd = 2 * d.x @ d.x_partials + 2 * d.y @ d.y_partials
+    np.testing.assert_allclose(g_rev, g_fwd, atol=1e-3)
+    np.testing.assert_array_equal(d.s, d.y)  # src/AutoDiff.jl:112 quirk kept
+    np.testing.assert_array_equal(d.s_value_true, sol.s)
+
+
+@pytest.mark.gpu
+def test_pullback_is_the_oracles_through_the_theta_map(gpu, oracle_lib):
+    """Alternative (K-form) constructor, batched θ: the API pullback is the kernel's
+    θ'-pullback (bit-exact vs the oracle) chained through ThetaMap.vjp."""
+    from mcp_amd.autodiff import solve_pullback
+
+    mcp = alternative_mcp()
+    rng = np.random.default_rng(8)
+    th = rng.standard_normal((16, 2))
+    sol = solve(InteriorPoint(), mcp, th, tol=1e-6)
+    gx, gy = rng.standard_normal((16, 2)), rng.standard_normal((16, 2))
+    dθ = solve_pullback(sol, gx, gy)
+    tp = mcp.theta_map(th)
+    ref, _ = oracle_lib.vjp_batch(0, 2, 2, tp, sol.x, sol.y, sol.s, gx, gy, None)
+    np.testing.assert_array_equal(dθ, mcp.theta_map.vjp(th, ref))
+
+
+@pytest.mark.gpu
+def test_torch_autograd_through_the_gpu_pullback(gpu):
+    import torch
+
+    from mcp_amd.autodiff import solve_pullback, solve_torch
+
+    mcp = basic_mcp()
+    th = torch.tensor([[-0.5, 0.5], [0.2, -0.1]], dtype=torch.float64, device="cuda", requires_grad=True)
+    x, y, s, status = solve_torch(mcp, th, tol=1e-6)
+    loss = (x ** 2).sum() + (y ** 2).sum()
+    loss.backward()
+    assert status.cpu().tolist() == [0, 0]
+    host = solve(InteriorPoint(), mcp, th.detach().cpu().numpy(), tol=1e-6)
+    ref = solve_pullback(host, 2 * host.x, 2 * host.y)
+    np.testing.assert_array_equal(th.grad.cpu().numpy(), ref)
