@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--linear-solver", default="schur", choices=["reduced", "dense", "schur"])
     ap.add_argument("--cpu-sample", type=int, default=32768, help="instances in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--sens", action="store_true",
+                    help="BASELINE C5: each step is the batched solve + the rrule pullback (VJP kernel) of "
+                         "f = Σx² + Σy² (src/AutoDiff.jl:42-82, test/runtests.jl:72-75)")
     ap.add_argument("--gather", action="store_true",
                     help="run the RCCL result collection even at world size 1 (rehearsal under torchrun)")
     return ap.parse_args()
@@ -145,8 +148,27 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
 
+    if a.sens:
+        from mcp_amd.batch import vjp_batch_device
+
+        p = theta.shape[1]
+        dtheta = torch.empty(B, p, dtype=torch.float64, device=dev)
+        vstat = torch.empty(B, dtype=torch.int32, device=dev)
+        zeros_m = torch.zeros(B, m, dtype=torch.float64, device=dev)
+        gx = torch.empty(B, n, dtype=torch.float64, device=dev)
+        gy = torch.empty(B, m, dtype=torch.float64, device=dev)
+
+    def pullback():
+        # cotangent of f = Σx² + Σy² (test/runtests.jl:72-75): ∂x = 2x, ∂y = 2y, ∂s = 0
+        torch.mul(out["x"], 2.0, out=gx)
+        torch.mul(out["y"], 2.0, out=gy)
+        vjp_batch_device(0, n, m, theta, out["x"], out["y"], out["s"], gx, gy, zeros_m, dtheta, vstat,
+                         stream=stream)
+
     def step():
         solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
+        if a.sens:
+            pullback()
         if gather is not None:
             gather()
 
@@ -156,12 +178,17 @@ def main():
     if distributed:
         dist.barrier()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(a.steps):
         ev[i][0].record(stream)
         solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
         ev[i][1].record(stream)
+        if a.sens:
+            evs[i][0].record(stream)
+            pullback()
+            evs[i][1].record(stream)
         if gather is not None:
             gather()
     torch.cuda.synchronize(dev)
@@ -169,6 +196,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    vjp_ms = float(np.mean([s.elapsed_time(e) for s, e in evs])) if a.sens else None
     # PCIe-inclusive rate of the host-buffer API (mcpx_solve_batch: H→D θ, solve, D→H
     # results) — reported beside `value`, never as it
     host_rate = None
@@ -232,6 +260,23 @@ def main():
             "success_rate": solved,
             "host_api_solves_per_s": host_rate,
         }
+        if a.sens:
+            p = n * n + m * n + m + n
+            vbytes = B * 8 * (2 * p + 3 * N + 2 * N)  # θ read, ∂θ written, (x,y,s) + cotangents read
+            vflops = B * lu_flops(N)
+            res["config"]["workload"] = (f"BASELINE C5: batched solve + rrule pullback (VJP kernel) of f = Σx²+Σy², "
+                                         f"QP-KKT n={n} m={m} (KKT dim {N}), fp64, {B} instances per GPU, tol={a.tol:g}")
+            res["sensitivity"] = {
+                "vjp_kernel_ms": vjp_ms, "solve_kernel_ms": kern_ms,
+                "vjp_per_s": B / (vjp_ms * 1e-3),
+                "vjp_failed": int((vstat != 0).sum().item()),
+                "vjp_roofline": {"flops_per_launch": vflops, "achieved_tflops": vflops / (vjp_ms * 1e-3) / 1e12,
+                                 "frac_fp64": vflops / (vjp_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                                 "algorithmic_bytes": vbytes, "achieved_gbs": vbytes / (vjp_ms * 1e-3) / 1e9,
+                                 "frac_hbm": vbytes / (vjp_ms * 1e-3) / 8.0e12,
+                                 "note": "one dense LU of the N-dim ∇F_zᵀ (2N³/3+2N²) per instance; bytes = θ read + "
+                                         "∂θ written + z and cotangents"},
+            }
         if world == 1 and a.cpu_sample > 0:
             th = int(a.cpu_threads) or min(16, os.cpu_count() or 1)
             res["cpu_baseline"] = cpu_baseline(theta_host[: a.cpu_sample], n, m, a.tol, th, a.linear_solver)
