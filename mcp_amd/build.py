@@ -10,9 +10,12 @@ the oracle.  hipcc cross-compiles for gfx950 without a GPU present.
 
 from __future__ import annotations
 
+import glob
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -48,9 +51,11 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     t0 = time.time()
     objs, procs = [], []
     jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 1)
+    tmp_dir = tempfile.mkdtemp(prefix="mcpx_build_")
     for src in SOURCES:  # one hipcc per translation unit, `jobs` at a time
-        obj = os.path.join(CSRC, os.path.basename(src) + (".alt" if out else "") + ".o")
-        cmd = [HIPCC, *FLAGS, *extra_flags, "-c", src, "-o", obj]
+        obj = os.path.join(tmp_dir, os.path.basename(src) + ".o")
+        # -save-temps=obj keeps the device .s next to the object for the hazard check
+        cmd = [HIPCC, *FLAGS, *extra_flags, "-save-temps=obj", "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd))
@@ -60,11 +65,19 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     for p, src in zip(procs, SOURCES):
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, f"hipcc {src}")
+    # hipcc does not pad hazards whose reader sits inside inline asm: refuse a build in
+    # which a compiler-placed VALU write feeds a DPP / cross-lane asm read too early
+    checker = os.path.join(ROOT, "tools", "check_dpp_hazards.py")
+    for asm in sorted(glob.glob(os.path.join(tmp_dir, "*amdgcn*gfx950.s"))):
+        r = subprocess.run([sys.executable, checker, asm], capture_output=True, text=True)
+        if verbose:
+            print(f"{os.path.basename(asm)}: {r.stdout.strip().splitlines()[-1]}", flush=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"inline-asm hazard in {asm}:\n{r.stdout[-2000:]}")
     tmp = lib_path + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
     os.replace(tmp, lib_path)
-    for o in objs:
-        os.remove(o)
+    shutil.rmtree(tmp_dir, ignore_errors=True)
     if verbose:
         print(f"built {lib_path} in {time.time() - t0:.1f}s", flush=True)
     return lib_path

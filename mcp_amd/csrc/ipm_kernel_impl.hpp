@@ -34,6 +34,25 @@
 
 #include "ipm_kernel.h"
 
+// A DPP read of a VGPR needs 2 wait states after a VALU write of it, and hipcc
+// does not pad hazards whose reader is inside an asm statement: a register copy
+// it places right before a DPP fmac would feed the fmac a stale source
+// (tools/check_dpp_hazards.py finds them in the .s).  MCPX_DPP_PAD pads each
+// DPP fmac with the 2 states.
+#ifndef MCPX_DPP_PAD_ON
+#define MCPX_DPP_PAD_ON 1
+#endif
+#if MCPX_DPP_PAD_ON
+#define MCPX_DPP_PAD "s_nop 1\n"
+#else
+#define MCPX_DPP_PAD ""
+#endif
+
+// Waves per SIMD the register allocator targets in the SCHUR fast pass (A/B knob).
+#ifndef MCPX_FAST_WAVES
+#define MCPX_FAST_WAVES 5
+#endif
+
 // Diagnostic phase stamps (tools/phase_profile.hip builds with MCPX_STAMPS=1;
 // the product build compiles them away).
 #ifndef MCPX_STAMPS
@@ -494,7 +513,7 @@ __device__ __forceinline__ void col_quot_nt2(double v0, double v1, double piv, d
 // distribution and the division lie between (≥ 2 wait states).
 #define MCPX_FMAC_NB(R)                                                                      \
   case R:                                                                                    \
-    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"  \
+    asm volatile(MCPX_DPP_PAD "v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"  \
                  : "+v"(acc) : "v"(src), "v"(nl));                                           \
     break;
 template <int R>
@@ -511,7 +530,7 @@ __device__ __forceinline__ void fmac_row_bcast(double& acc, double src, double n
 // happens before the write, so every lane sees the pivot lane's old value).
 #define MCPX_FMAC_NB_SELF(R)                                                                 \
   case R:                                                                                    \
-    asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"  \
+    asm volatile(MCPX_DPP_PAD "v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"  \
                  : "+v"(acc) : "v"(nl));                                                     \
     break;
 template <int R>
@@ -731,7 +750,7 @@ __device__ __forceinline__ void schur_rows_from_2d(const d4 (&acc)[NT][NT], int 
 //      deterministic, so they end bit-identical to a single complete pass); all
 //      others exit at once.
 template <int NMAX, int FAMILY, int NC, int MC, int SOLVER, int PASS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 5 : 1, 8))) void ipm_solve_kernel(const KernelArgs args) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? MCPX_FAST_WAVES : 1, 8))) void ipm_solve_kernel(const KernelArgs args) {
   constexpr bool RED = SOLVER != MCPX_LINSOLVE_DENSE;  // lanes [0,n) x, [n,n+m) (y, s)
   constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR;
   static_assert(SCH || PASS == 0, "two-pass launch is for the SCHUR solver only");
