@@ -31,6 +31,10 @@
  *                       column-major, p = n² + 2 n m + m² + n + m.
  *                       (The Python front-end traces user G/H callables —
  *                       src/mcp.jl:27-52, :155-210 — into this layout.)
+ *   MCPX_FAMILY_NONLINEAR  general G(x,y;θ), H(x,y;θ) (e.g. the trajectory games of
+ *                       src/game.jl): device code generated per problem and run
+ *                       through an mcpx_module (end of this header); θ is the
+ *                       problem's own parameter vector.
  *
  * Conventions: all arrays are instance-major (instance b's data is contiguous,
  * stride `theta_ld` for θ); all buffers are caller-owned; the library keeps no
@@ -48,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MCPX_VERSION 10100 /* 1.1.0 */
+#define MCPX_VERSION 10200 /* 1.2.0 */
 
 /* error codes */
 #define MCPX_OK 0
@@ -63,6 +67,7 @@ extern "C" {
 
 #define MCPX_FAMILY_QP 0
 #define MCPX_FAMILY_AFFINE 1
+#define MCPX_FAMILY_NONLINEAR 2
 
 /* largest linear-system dimension of the register-resident kernels
  * (n + m for MCPX_LINSOLVE_REDUCED, n + 2m for MCPX_LINSOLVE_DENSE) */
@@ -205,6 +210,35 @@ int mcpx_jvp_batch(const mcpx_desc* desc, const double* theta, const double* x, 
 int mcpx_jvp_batch_device(const mcpx_desc* desc, const double* theta, const double* x,
                           const double* y, const double* s, int32_t n_partials,
                           const double* theta_dot, double* zdot, int32_t* status, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Nonlinear G/H — MCPX_FAMILY_NONLINEAR (BASELINE C4: games, src/game.jl).
+ *
+ * The reference compiles F!/∇F_z! from Symbolics expressions once per problem
+ * (build_function, src/mcp.jl:82-120).  The front-end does the same for the
+ * GPU (mcp_amd/codegen.py): straight-line device code for G, H and their
+ * Jacobian blocks, compiled with the solver template
+ * (mcp_amd/csrc/ipm_nl_kernel.hpp) into one gfx950 code object per problem.
+ * These calls load and run it.  A module holds the kernels its size admits:
+ * MCPX_LINSOLVE_SCHUR (∂H/∂y ≡ 0, n ≤ 64, m ≤ 128), _REDUCED (n + m ≤ 64),
+ * _DENSE (n + 2m ≤ 64); another linear_solver is MCPX_EUNSUPPORTED.
+ */
+typedef struct mcpx_module mcpx_module;
+/* Loads the code object at `path` on the current device (other devices load
+ * it on first use).  No usable GPU: MCPX_ENODEV. */
+int mcpx_module_load(const char* path, mcpx_module** mod);
+/* The module's n, m, θ dimension p and kernel mask (bit MCPX_LINSOLVE_*);
+ * NULL pointers are skipped. */
+int mcpx_module_dims(const mcpx_module* mod, int32_t* n, int32_t* m, int32_t* p, int32_t* solvers);
+void mcpx_module_unload(mcpx_module* mod);
+/* mcpx_solve_batch / mcpx_solve_batch_device for the module's problem:
+ * desc->family = MCPX_FAMILY_NONLINEAR, desc->n / m = the module's, theta_ld >= p. */
+int mcpx_solve_batch_module(mcpx_module* mod, const mcpx_desc* desc, const double* theta,
+                            const double* x0, const double* y0, const double* s0,
+                            const mcpx_params* prm, int num_devices, mcpx_out* out);
+int mcpx_solve_batch_module_device(mcpx_module* mod, const mcpx_desc* desc, const double* theta,
+                                   const double* x0, const double* y0, const double* s0,
+                                   const mcpx_params* prm, const mcpx_out* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,7 @@ STATUS_FAILED = 1
 
 FAMILY_QP = 0
 FAMILY_AFFINE = 1
+FAMILY_NONLINEAR = 2  # generated device code per problem (mcp_amd/codegen.py)
 
 MAX_KKT_DIM = 64
 JVP_RHS = 8  # MCPX_JVP_RHS: partials per factorisation of the JVP kernel
@@ -92,4 +93,6 @@ def theta_dim(family: int, n: int, m: int) -> int:
         return n * n + m * n + m + n
     if family == FAMILY_AFFINE:
         return n * n + 2 * n * m + m * m + n + m
+    if family == FAMILY_NONLINEAR:
+        raise ValueError("a nonlinear MCP's θ dimension is its own (NLSystem.p, mcpx_module_dims)")
     raise ValueError(f"unknown family {family}")

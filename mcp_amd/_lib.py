@@ -27,7 +27,8 @@ class MCPXError(RuntimeError):
 
 EXPORTS = ("mcpx_version", "mcpx_last_error", "mcpx_default_params", "mcpx_theta_dim",
            "mcpx_device_count", "mcpx_solve_batch", "mcpx_solve_batch_device", "mcpx_vjp_batch",
-           "mcpx_vjp_batch_device", "mcpx_jvp_batch", "mcpx_jvp_batch_device")
+           "mcpx_vjp_batch_device", "mcpx_jvp_batch", "mcpx_jvp_batch_device", "mcpx_module_load",
+           "mcpx_module_dims", "mcpx_module_unload", "mcpx_solve_batch_module", "mcpx_solve_batch_module_device")
 
 
 def lib():
@@ -61,6 +62,19 @@ def lib():
     L.mcpx_jvp_batch.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, C.c_int, P, P]
     L.mcpx_jvp_batch_device.restype = C.c_int
     L.mcpx_jvp_batch_device.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, P, P, P]
+    I32P = C.POINTER(C.c_int32)
+    L.mcpx_module_load.restype = C.c_int
+    L.mcpx_module_load.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]
+    L.mcpx_module_dims.restype = C.c_int
+    L.mcpx_module_dims.argtypes = [C.c_void_p, I32P, I32P, I32P, I32P]
+    L.mcpx_module_unload.restype = None
+    L.mcpx_module_unload.argtypes = [C.c_void_p]
+    L.mcpx_solve_batch_module.restype = C.c_int
+    L.mcpx_solve_batch_module.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P, C.POINTER(_abi.Params),
+                                          C.c_int, C.POINTER(_abi.Out)]
+    L.mcpx_solve_batch_module_device.restype = C.c_int
+    L.mcpx_solve_batch_module_device.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P,
+                                                 C.POINTER(_abi.Params), C.POINTER(_abi.Out), C.c_void_p]
     _lib = L
     return L
 

@@ -16,9 +16,13 @@ gfx950 kernels evaluate on device per instance (include/mcpx.h):
 The coefficients may depend on θ arbitrarily; the θ → θ' map is compiled into
 a sparse linear part (gathers/scaled adds, which is what every benchmark family
 is) plus lambdified residual expressions, and is evaluated per batch with numpy
-(host θ) or torch (device θ).  G/H that are not affine in (x, y) — the
-reference's nonlinear games, e.g. examples/lane_change.jl — need on-device
-codegen of general F/∇F and raise NotImplementedError.
+(host θ) or torch (device θ).
+
+* MCPX_FAMILY_NONLINEAR  any other G/H — e.g. the reference's trajectory
+                      games (examples/lane_change.jl): G, H and their Jacobian
+                      blocks become device code generated per problem
+                      (mcp_amd/codegen.py, the build_function analogue), which
+                      the kernel evaluates every Newton step; θ' = θ.
 
 solve() keeps the reference's keyword arguments and result fields
 (src/solver.jl:35-51,121), including the in-place update of caller-supplied
@@ -64,7 +68,7 @@ def _as_exprs(v, what: str) -> list:
 
 
 class NotAffineError(NotImplementedError):
-    """G/H not affine in (x, y): needs the general on-device F/∇F codegen (SURVEY.md §8(f) #2)."""
+    """G/H not affine in (x, y): the MCP goes to the nonlinear family (generated device code)."""
 
 
 def _affine_rows(rows: list, zs: list, what: str):
@@ -305,7 +309,7 @@ class PrimalDualMCP:
             ys = make_variables("y", constrained_dimension)
             ts = make_variables("θ", parameter_dimension)
             self._init_symbolic(_as_exprs(G(xs, ys, θ=ts), "G"), _as_exprs(H(xs, ys, θ=ts), "H"),
-                                list(xs), list(ys), list(ts), compute_sensitivities)
+                                list(xs), list(ys), list(ts), compute_sensitivities, backend_options)
         elif len(args) == 3 and callable(args[0]):
             K, lo, hi = args
             if parameter_dimension is None:
@@ -313,7 +317,8 @@ class PrimalDualMCP:
                                 "needs parameter_dimension")
             zs = make_variables("z", len(lo))
             ts = make_variables("θ", parameter_dimension)
-            self._init_K(_as_exprs(K(zs, θ=ts), "K"), list(zs), list(ts), lo, hi, compute_sensitivities)
+            self._init_K(_as_exprs(K(zs, θ=ts), "K"), list(zs), list(ts), lo, hi, compute_sensitivities,
+                         backend_options)
         elif len(args) == 0:
             pass  # used by the from_symbolic* class methods
         else:
@@ -326,7 +331,7 @@ class PrimalDualMCP:
                       compute_sensitivities=True, backend_options=None) -> "PrimalDualMCP":
         self = cls()
         self._init_symbolic(_as_exprs(G_symbolic, "G"), _as_exprs(H_symbolic, "H"), list(x_symbolic),
-                            list(y_symbolic), list(θ_symbolic), compute_sensitivities)
+                            list(y_symbolic), list(θ_symbolic), compute_sensitivities, backend_options)
         return self
 
     @classmethod
@@ -334,10 +339,10 @@ class PrimalDualMCP:
                         compute_sensitivities=True, backend_options=None) -> "PrimalDualMCP":
         self = cls()
         self._init_K(_as_exprs(K_symbolic, "K"), list(z_symbolic), list(θ_symbolic), lower_bounds, upper_bounds,
-                     compute_sensitivities)
+                     compute_sensitivities, backend_options)
         return self
 
-    def _init_K(self, K, zs, ts, lower_bounds, upper_bounds, compute_sensitivities):
+    def _init_K(self, K, zs, ts, lower_bounds, upper_bounds, compute_sensitivities, backend_options=None):
         lo = np.asarray(lower_bounds, dtype=float)
         hi = np.asarray(upper_bounds, dtype=float)
         # src/mcp.jl:191 — the reference @asserts this
@@ -348,9 +353,9 @@ class PrimalDualMCP:
         unc = [i for i in range(len(zs)) if np.isinf(lo[i])]
         con = [i for i in range(len(zs)) if not np.isinf(lo[i])]
         self._init_symbolic([K[i] for i in unc], [K[i] for i in con], [zs[i] for i in unc], [zs[i] for i in con],
-                            ts, compute_sensitivities)
+                            ts, compute_sensitivities, backend_options)
 
-    def _init_symbolic(self, G, H, xs, ys, ts, compute_sensitivities):
+    def _init_symbolic(self, G, H, xs, ys, ts, compute_sensitivities, backend_options=None):
         sp = _sp()
         n, m = len(xs), len(ys)
         if len(G) != n or len(H) != m:
@@ -363,8 +368,20 @@ class PrimalDualMCP:
         self.G_symbolic, self.H_symbolic = G, H
         self.x_symbolic, self.y_symbolic, self.θ_symbolic = xs, ys, ts
         zs = xs + ys
-        CG, cg = _affine_rows(G, zs, "G")
-        CH, ch = _affine_rows(H, zs, "H")
+        self.nl = None
+        self._module = None
+        try:
+            if (backend_options or {}).get("family") == "nonlinear":  # force the generated-code path
+                raise NotAffineError("nonlinear family requested through backend_options")
+            CG, cg = _affine_rows(G, zs, "G")
+            CH, ch = _affine_rows(H, zs, "H")
+        except NotAffineError:
+            from . import codegen
+
+            self.family = _abi.FAMILY_NONLINEAR
+            self.nl = codegen.NLSystem(G, H, xs, ys, ts)
+            self.theta_map = ThetaMap(list(ts), ts)  # θ' = θ
+            return
         P = [[CG[i][j] for j in range(n)] for i in range(n)]
         Q = [[CG[i][n + k] for k in range(m)] for i in range(n)]
         R = [[CH[k][j] for j in range(n)] for k in range(m)]
@@ -381,6 +398,28 @@ class PrimalDualMCP:
         self.theta_map = ThetaMap(exprs, ts)
         assert self.theta_map.p_out == _abi.theta_dim(self.family, n, m)
 
+    def module(self):
+        """The loaded gfx950 code object of a nonlinear-family MCP: compiled on first
+        use (cached in-tree by content hash, mcp_amd/_gen), loaded once per process."""
+        if self.nl is None:
+            raise TypeError("only nonlinear-family MCPs have a generated module")
+        if self._module is None:
+            from .batch import Module
+
+            self._module = Module(self.nl.build_module())
+        return self._module
+
+    def _nl_host(self):
+        """Lambdified (G; H) and its z-Jacobian: host inspection of a nonlinear MCP."""
+        if getattr(self, "_nl_fns", None) is None:
+            sp = _sp()
+            zs = list(self.x_symbolic) + list(self.y_symbolic)
+            args = zs + list(self.θ_symbolic)
+            GH = list(self.G_symbolic) + list(self.H_symbolic)
+            self._nl_fns = (sp.lambdify(args, GH, "numpy"),
+                            sp.lambdify(args, sp.Matrix(GH).jacobian(zs), "numpy"))
+        return self._nl_fns
+
     # -- host evaluation of the reference callbacks (inspection / tests) ----
     def family_parameters(self, θ):
         """θ → θ' (the per-instance data the kernel reads), numpy or torch."""
@@ -388,6 +427,8 @@ class PrimalDualMCP:
 
     def blocks(self, θ):
         """Affine blocks (P, Q, R, S, g, h) of G = P x + Q y + g, H = R x + S y + h at one θ."""
+        if self.family == _abi.FAMILY_NONLINEAR:
+            raise TypeError("a nonlinear MCP has no constant affine blocks; see F / jacobian_z")
         n, m = self.unconstrained_dimension, self.constrained_dimension
         t = self.theta_map(np.asarray(θ, float).reshape(1, -1))[0]
         if self.family == _abi.FAMILY_QP:
@@ -405,22 +446,31 @@ class PrimalDualMCP:
 
     def F(self, x, y, s, *, θ, ϵ):
         """F(x, y, s; θ, ϵ) = [G; H − s; s⊙y − ϵ] (src/mcp.jl:72-80), host numpy."""
-        P, Q, R, S, g, h = self.blocks(θ)
         x, y, s = (np.asarray(v, float) for v in (x, y, s))
+        if self.family == _abi.FAMILY_NONLINEAR:
+            n = self.unconstrained_dimension
+            gh = np.asarray(self._nl_host()[0](*x, *y, *np.asarray(θ, float)), float).reshape(-1)
+            return np.concatenate([gh[:n], gh[n:] - s, s * y - ϵ])
+        P, Q, R, S, g, h = self.blocks(θ)
         return np.concatenate([P @ x + Q @ y + g, R @ x + S @ y + h - s, s * y - ϵ])
 
     def jacobian_z(self, x, y, s, *, θ, ϵ=None):
         """∇F_z (src/mcp.jl:97-120) as a dense N×N host array."""
-        P, Q, R, S, g, h = self.blocks(θ)
         n, m = self.unconstrained_dimension, self.constrained_dimension
         J = np.zeros((n + 2 * m, n + 2 * m))
-        J[:n, :n], J[:n, n:n + m] = P, Q
-        J[n:n + m, :n], J[n:n + m, n:n + m], J[n:n + m, n + m:] = R, S, -np.eye(m)
+        if self.family == _abi.FAMILY_NONLINEAR:
+            J[:n + m, :n + m] = np.asarray(self._nl_host()[1](*np.asarray(x, float), *np.asarray(y, float),
+                                                              *np.asarray(θ, float)), float).reshape(n + m, n + m)
+            J[n:n + m, n + m:] = -np.eye(m)
+        else:
+            P, Q, R, S, g, h = self.blocks(θ)
+            J[:n, :n], J[:n, n:n + m] = P, Q
+            J[n:n + m, :n], J[n:n + m, n:n + m], J[n:n + m, n + m:] = R, S, -np.eye(m)
         J[n + m:, n:n + m], J[n + m:, n + m:] = np.diag(np.asarray(s, float)), np.diag(np.asarray(y, float))
         return J
 
     def __repr__(self):
-        fam = {_abi.FAMILY_QP: "qp", _abi.FAMILY_AFFINE: "affine"}[self.family]
+        fam = {_abi.FAMILY_QP: "qp", _abi.FAMILY_AFFINE: "affine", _abi.FAMILY_NONLINEAR: "nonlinear"}[self.family]
         return (f"PrimalDualMCP(n={self.unconstrained_dimension}, m={self.constrained_dimension}, "
                 f"parameter_dimension={self.parameter_dimension}, family={fam})")
 
@@ -467,6 +517,8 @@ _STATUS = np.array(["solved", "failed"])
 
 def _linear_solver(mcp: PrimalDualMCP, linear_solve_algorithm) -> str:
     if linear_solve_algorithm is None:
+        if mcp.family == _abi.FAMILY_NONLINEAR:
+            return mcp.nl.default_solver()
         return "schur" if mcp.family == _abi.FAMILY_QP else "reduced"
     if isinstance(linear_solve_algorithm, str):
         if linear_solve_algorithm not in _abi.LINEAR_SOLVERS:
@@ -521,7 +573,7 @@ def solve(solver_type, mcp=None, θ=None, *, x0=None, y0=None, s0=None, tol=1e-4
     tp = mcp.theta_map(th)
     B = tp.shape[0]
     r = solve_batch(mcp.family, n, m, tp, x0=x0, y0=y0, s0=s0, params=prm, num_devices=num_devices,
-                    trace_len=trace_len)
+                    trace_len=trace_len, module=mcp.module() if mcp.nl is not None else None)
     if verbose:
         for b in np.nonzero(r["status"] != 0)[0][:16]:
             warnings.warn(f"instance {b}: Newton linear solve or line search failed "
@@ -549,7 +601,8 @@ def _solve_device(mcp, θ, prm, x0, y0, s0, trace_len):
     th = θ if θ.dim() == 2 else θ[None, :]
     tp = mcp.theta_map(th)
     n, m = mcp.unconstrained_dimension, mcp.constrained_dimension
-    out = solve_batch_device(mcp.family, n, m, tp, x0=x0, y0=y0, s0=s0, params=prm, trace_len=trace_len)
+    out = solve_batch_device(mcp.family, n, m, tp, x0=x0, y0=y0, s0=s0, params=prm, trace_len=trace_len,
+                             module=mcp.module() if mcp.nl is not None else None)
     return MCPSolution(out["status"], out["x"], out["y"], out["s"], out["kkt_error"], out["eps"],
                        out["outer_iters"], out.get("newton_iters"), out.get("active_mask"),
                        out.get("alpha_trace"), θ=th, params=prm, mcp=mcp)
@@ -621,7 +674,8 @@ class ParametricGame:
       L_i = f_i − λ_iᵀ g_i − μ_iᵀ h_i − λ̃ᵀ g̃ − μ̃ᵀ h̃,
       lower bounds −Inf for x, λ, λ̃ and 0 for μ, μ̃."""
 
-    def __init__(self, *, test_point, test_parameter, problems, shared_equality=None, shared_inequality=None):
+    def __init__(self, *, test_point, test_parameter, problems, shared_equality=None, shared_inequality=None,
+                 backend_options=None):
         sp = _sp()
         self.problems = list(problems)
         self.shared_equality = shared_equality
@@ -665,7 +719,7 @@ class ParametricGame:
         nx, nl, nls, nm, nms = len(x), len(lam), len(lam_s), len(mu), len(mu_s)
         lo = [-math.inf] * (nx + nl + nls) + [0.0] * (nm + nms)
         hi = [math.inf] * len(z)
-        self.mcp = PrimalDualMCP.from_symbolic_K(K, z, list(th.data), lo, hi)
+        self.mcp = PrimalDualMCP.from_symbolic_K(K, z, list(th.data), lo, hi, backend_options=backend_options)
 
     def _dimensions(self, tp: BlockVector, tt: BlockVector) -> dict:
         """src/game.jl:159-187 (evaluated numerically on the test point)."""

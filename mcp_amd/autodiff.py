@@ -41,6 +41,9 @@ class NoTangent:
 
 
 def _require_sensitivities(mcp) -> None:
+    if getattr(mcp, "nl", None) is not None:
+        raise NotImplementedError("sensitivities of nonlinear-family MCPs (generated ∇F_θ code and a ≥ 90-dim "
+                                  "adjoint solve for the lane-change game) are not built yet (DESIGN.md §10)")
     # src/AutoDiff.jl:19-23
     if not getattr(mcp, "compute_sensitivities", False):
         raise ValueError("Missing sensitivities. Set `compute_sensitivities = True` when constructing the "

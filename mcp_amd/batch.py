@@ -15,6 +15,7 @@ Both return the per-instance fields of the reference's result NamedTuple
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -30,8 +31,28 @@ def _params(params=None, **kw) -> _abi.Params:
     return params if params is not None else _abi.make_params(**kw)
 
 
+class Module:
+    """A generated nonlinear-MCP code object (mcp_amd/codegen.py) loaded through
+    the C ABI (mcpx_module_load, include/mcpx.h MCPX_FAMILY_NONLINEAR).  Kept for
+    the process lifetime unless close() is called."""
+
+    def __init__(self, path: str):
+        h = C.c_void_p()
+        check(lib().mcpx_module_load(os.fsencode(path), C.byref(h)))
+        self.handle = h
+        v = [C.c_int32() for _ in range(4)]
+        check(lib().mcpx_module_dims(h, *(C.byref(x) for x in v)))
+        self.n, self.m, self.p, self.solvers = (x.value for x in v)
+        self.path = path
+
+    def close(self) -> None:
+        if self.handle:
+            lib().mcpx_module_unload(self.handle)
+            self.handle = None
+
+
 def solve_batch(family: int, n: int, m: int, theta, *, x0=None, y0=None, s0=None, params=None,
-                num_devices: int = 0, trace_len: int = 0, **kw) -> dict:
+                num_devices: int = 0, trace_len: int = 0, module: Module | None = None, **kw) -> dict:
     """Solve B instances on the GPU(s).  theta: (B, ≥p) float64 host array."""
     theta = np.ascontiguousarray(theta, dtype=np.float64)
     if theta.ndim == 1:
@@ -53,8 +74,12 @@ def solve_batch(family: int, n: int, m: int, theta, *, x0=None, y0=None, s0=None
                    _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
                    int(trace_len), 0)
     desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
-    check(lib().mcpx_solve_batch(C.byref(desc), _ptr(theta), _ptr(x0), _ptr(y0), _ptr(s0),
-                                 C.byref(prm), int(num_devices), C.byref(out)))
+    if module is not None:  # MCPX_FAMILY_NONLINEAR: the problem's generated code object
+        check(lib().mcpx_solve_batch_module(module.handle, C.byref(desc), _ptr(theta), _ptr(x0), _ptr(y0),
+                                            _ptr(s0), C.byref(prm), int(num_devices), C.byref(out)))
+    else:
+        check(lib().mcpx_solve_batch(C.byref(desc), _ptr(theta), _ptr(x0), _ptr(y0), _ptr(s0),
+                                     C.byref(prm), int(num_devices), C.byref(out)))
     return r
 
 
@@ -75,7 +100,8 @@ def alloc_device_outputs(B: int, n: int, m: int, device, trace_len: int = 0, new
 
 
 def solve_batch_device(family: int, n: int, m: int, theta, out: dict | None = None, *, x0=None, y0=None,
-                       s0=None, params=None, trace_len: int = 0, stream=None, **kw) -> dict:
+                       s0=None, params=None, trace_len: int = 0, stream=None, module: Module | None = None,
+                       **kw) -> dict:
     """Enqueue a batched solve on torch device tensors (no synchronisation).
 
     theta: (B, ≥p) contiguous float64 CUDA(HIP) tensor.  `out` (from
@@ -100,8 +126,12 @@ def solve_batch_device(family: int, n: int, m: int, theta, out: dict | None = No
     prm = _params(params, **kw)
     desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
     st = stream if stream is not None else torch.cuda.current_stream(theta.device)
-    check(lib().mcpx_solve_batch_device(C.byref(desc), dp(theta), dp(x0), dp(y0), dp(s0), C.byref(prm),
-                                        C.byref(o), C.c_void_p(st.cuda_stream)))
+    if module is not None:
+        check(lib().mcpx_solve_batch_module_device(module.handle, C.byref(desc), dp(theta), dp(x0), dp(y0), dp(s0),
+                                                   C.byref(prm), C.byref(o), C.c_void_p(st.cuda_stream)))
+    else:
+        check(lib().mcpx_solve_batch_device(C.byref(desc), dp(theta), dp(x0), dp(y0), dp(s0), C.byref(prm),
+                                            C.byref(o), C.c_void_p(st.cuda_stream)))
     return out
 
 

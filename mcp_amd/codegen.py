@@ -1,0 +1,316 @@
+"""Device code generation for general (nonlinear) G/H — MCPX_FAMILY_NONLINEAR.
+
+The reference compiles F!, ∇F_z! (and ∇F_θ!) from Symbolics expressions with
+`build_function` once per problem (src/mcp.jl:82-120).  This module is that
+step for the GPU: it turns the traced G(x, y; θ), H(x, y; θ) into straight-line
+C that both the gfx950 kernel (hipcc, compiled with the solver template
+csrc/ipm_nl_kernel.hpp into a code object the C ABI loads with
+`mcpx_module_load`) and the CPU oracle (gcc, tests only) compile from the very
+same text, so the evaluation order — and with -ffp-contract=off every
+rounding — is identical on both sides.
+
+Generated functions (MCPX_NL_FN is `__device__` on the GPU, `static inline` in C):
+
+  mcpx_nl_init(th, blk)      the Jacobian entries that do not depend on z
+                             (θ-only and constant entries — the reference's
+                             `constant_entries`, src/mcp.jl:111-112), once per
+                             instance;
+  mcpx_nl_eval(th, z, blk)   G, H and the z-dependent Jacobian entries at
+                             z = [x; y], once per Newton step.
+
+Block layout of `blk` (doubles, column-major blocks like the affine family):
+
+  P = ∂G/∂x  n×n  at OFF_P = 0              P[i, j] = blk[j·n + i]
+  Q = ∂G/∂y  n×m  at OFF_Q = n²             Q[i, k] = blk[OFF_Q + k·n + i]
+  R = ∂H/∂x  m×n  at OFF_R = n² + nm        R[k, j] = blk[OFF_R + j·m + k]
+  g = G      n    at OFF_G = n² + 2nm
+  h = H      m    at OFF_H = OFF_G + n
+  S = ∂H/∂y  m×m  at OFF_S = OFF_H + m      S[k, q] = blk[OFF_S + q·m + k]
+                  (written only when ∂H/∂y is not structurally zero: HAS_S)
+
+Structural zeros are never written (the kernel zeroes the block once).
+
+Op order: after common-subexpression elimination (sympy.cse) every node is
+printed fully parenthesised as a left fold over sympy's canonical argument
+order; integer powers become repeated products, x**-k a division of 1 by the
+product, x**(±1/2) sqrt; numbers are exact hex-float literals.  Polynomial and
+rational G/H are therefore bit-identical between GPU and oracle (+ − × ÷ and
+sqrt are correctly rounded on both); for transcendental functions (sin, exp, …)
+device libm (ocml) and glibc may differ by an ulp, and parity is then the
+north_star's 1e-8 bar only.
+"""
+
+from __future__ import annotations
+
+import glob
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+GEN_DIR = os.environ.get("MCPX_GEN_DIR") or os.path.join(HERE, "_gen")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+# bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
+GEN_VERSION = 1
+LDS_LIMIT = 160 * 1024 - 2048  # bytes of static LDS one workgroup may declare on gfx950 (minus headroom)
+
+_FUNCS = {  # sympy function → C name (both libm and HIP device math)
+    "sin": "sin", "cos": "cos", "tan": "tan", "exp": "exp", "log": "log", "tanh": "tanh",
+    "sinh": "sinh", "cosh": "cosh", "asin": "asin", "acos": "acos", "atan": "atan",
+    "Abs": "fabs", "atan2": "atan2",
+}
+
+
+def _sp():
+    import sympy
+
+    return sympy
+
+
+def _lit(v) -> str:
+    f = float(v)
+    if f != f or f in (float("inf"), float("-inf")):
+        raise ValueError(f"non-finite constant {v} in a generated expression")
+    s = f.hex()
+    return f"({s})" if f < 0 else s
+
+
+class _Printer:
+    """sympy expression → fully parenthesised C expression with a fixed op order."""
+
+    def __init__(self, names: dict):
+        self.names = names  # Symbol → C operand
+
+    def __call__(self, e) -> str:
+        sp = _sp()
+        if e in self.names:
+            return self.names[e]
+        if e.is_Number:
+            return _lit(e)
+        if e.is_Symbol:
+            raise ValueError(f"free symbol {e} is neither a decision variable nor a parameter")
+        if e.is_Add:
+            out = None
+            for t in e.as_ordered_terms():
+                neg = False
+                c, rest = t.as_coeff_Mul()
+                if c == -1 and rest != 1:
+                    neg, t = True, rest
+                s = self(t)
+                if out is None:
+                    out = f"(-{s})" if neg else s
+                else:
+                    out = f"({out} {'-' if neg else '+'} {s})"
+            return out
+        if e.is_Mul:
+            c, rest = e.as_coeff_Mul()
+            if c == -1:
+                return f"(-{self(rest)})"
+            facs = list(e.as_ordered_factors())
+            recip = lambda f: f.is_Pow and f.exp.is_Integer and f.exp < 0
+            num = [f for f in facs if not recip(f)]
+            den = [f.base ** (-f.exp) for f in facs if recip(f)]
+            out = None
+            for f in num:
+                s = self(f)
+                out = s if out is None else f"({out} * {s})"
+            if out is None:
+                out = _lit(1.0)
+            for f in den:  # x·y⁻ᵏ prints as a division by the product yᵏ
+                out = f"({out} / {self(f)})"
+            return out
+        if e.is_Pow:
+            b, x = e.base, e.exp
+            if x.is_Integer:
+                k = int(x)
+                if k == 0:
+                    return _lit(1.0)
+                bs = self(b)
+                prod = bs
+                for _ in range(abs(k) - 1):
+                    prod = f"({prod} * {bs})"
+                return prod if k > 0 else f"({_lit(1.0)} / {prod})"
+            if x == sp.Rational(1, 2):
+                return f"sqrt({self(b)})"
+            if x == sp.Rational(-1, 2):
+                return f"({_lit(1.0)} / sqrt({self(b)}))"
+            return f"pow({self(b)}, {self(x)})"
+        if isinstance(e, sp.Function):
+            name = type(e).__name__
+            if name not in _FUNCS:
+                raise NotImplementedError(f"function {name} has no generated-code mapping")
+            return f"{_FUNCS[name]}({', '.join(self(a) for a in e.args)})"
+        raise NotImplementedError(f"cannot generate code for {type(e).__name__}: {e}")
+
+
+class NLSystem:
+    """The generated evaluation code of one nonlinear PrimalDualMCP.
+
+    G (n), H (m): sympy expressions in the decision variables xs (n), ys (m)
+    and the parameters ts (p)."""
+
+    def __init__(self, G, H, xs, ys, ts):
+        sp = _sp()
+        self.n, self.m, self.p = len(xs), len(ys), len(ts)
+        n, m = self.n, self.m
+        self.G, self.H = [sp.sympify(e) for e in G], [sp.sympify(e) for e in H]
+        self.xs, self.ys, self.ts = list(xs), list(ys), list(ts)
+        zset = set(self.xs) | set(self.ys)
+        nn, nm = n * n, n * m
+        self.OFF_P, self.OFF_Q, self.OFF_R = 0, nn, nn + nm
+        self.OFF_G = nn + 2 * nm
+        self.OFF_H = self.OFF_G + n
+        self.OFF_S = self.OFF_H + m
+        const_entries, var_entries = [], []
+
+        def put(idx, e):
+            if e == 0:
+                return
+            (var_entries if (e.free_symbols & zset) else const_entries).append((idx, e))
+
+        for i, g in enumerate(self.G):
+            for j, xj in enumerate(self.xs):
+                put(self.OFF_P + j * n + i, sp.diff(g, xj))
+            for k, yk in enumerate(self.ys):
+                put(self.OFF_Q + k * n + i, sp.diff(g, yk))
+        S_entries = []
+        for k, h in enumerate(self.H):
+            for j, xj in enumerate(self.xs):
+                put(self.OFF_R + j * m + k, sp.diff(h, xj))
+            for q, yq in enumerate(self.ys):
+                d = sp.diff(h, yq)
+                if d != 0:
+                    S_entries.append((self.OFF_S + q * m + k, d))
+        self.has_s = bool(S_entries)
+        for idx, d in S_entries:
+            put(idx, d)
+        self.size = self.OFF_S + (m * m if self.has_s else 0)
+        self.const_entries = sorted(const_entries, key=lambda t: t[0])
+        self.var_entries = sorted(var_entries, key=lambda t: t[0])
+        # residual values: per step (they carry z)
+        self.residuals = ([(self.OFF_G + i, g) for i, g in enumerate(self.G)]
+                          + [(self.OFF_H + k, h) for k, h in enumerate(self.H)])
+        self.nnz = len(self.const_entries) + len(self.var_entries)
+        self.body = self._emit()
+        self.key = hashlib.sha256(f"v{GEN_VERSION}\n{self.body}".encode()).hexdigest()[:24]
+
+    # ---- which one-wave kernels the module gets (csrc/ipm_nl_kernel.hpp) -------
+    def schur_lds_bytes(self) -> int:
+        n, m = self.n, self.m
+        return 8 * (self.OFF_S + m * n + 3 * (n + 2 * m) + 4 * m)
+
+    def solvers(self) -> dict:
+        n, m = self.n, self.m
+        return {
+            "schur": (not self.has_s) and 1 <= n <= 64 and m <= 128 and self.schur_lds_bytes() <= LDS_LIMIT,
+            "reduced": 1 <= n + m <= 64,
+            "dense": 1 <= n + 2 * m <= 64,
+        }
+
+    def default_solver(self) -> str:
+        ok = self.solvers()
+        for s in ("schur", "reduced", "dense"):
+            if ok[s]:
+                return s
+        raise NotImplementedError(
+            f"nonlinear MCP with n={self.n}, m={self.m} exceeds the one-wave kernels (schur: dH/dy = 0, "
+            f"n <= 64, m <= 128; reduced: n + m <= 64; dense: n + 2m <= 64) — the workgroup-per-instance "
+            f"blocked LU is SURVEY.md §8(f) #2's remaining half")
+
+    # ---- emission ------------------------------------------------------------
+    def _block(self, entries, with_z: bool) -> list:
+        sp = _sp()
+        names = {t: f"th[{k}]" for k, t in enumerate(self.ts)}
+        if with_z:
+            names.update({x: f"z[{j}]" for j, x in enumerate(self.xs)})
+            names.update({y: f"z[{self.n + k}]" for k, y in enumerate(self.ys)})
+        if not entries:
+            return []
+        reps, red = sp.cse([e for _, e in entries], symbols=sp.numbered_symbols("c"), order="canonical")
+        pr = _Printer(names)
+        lines = []
+        for sym, e in reps:
+            lines.append(f"  const double {sym} = {pr(e)};")
+            names[sym] = str(sym)
+        for (idx, _), e in zip(entries, red):
+            lines.append(f"  blk[{idx}] = {pr(e)};")
+        return lines
+
+    def _emit(self) -> str:
+        init = self._block(self.const_entries, with_z=False)
+        ev = self._block(self.var_entries + self.residuals, with_z=True)
+        return "\n".join([
+            "/* generated by mcp_amd/codegen.py — do not edit */",
+            f"#define MCPX_NL_N {self.n}",
+            f"#define MCPX_NL_M {self.m}",
+            f"#define MCPX_NL_P {self.p}",
+            f"#define MCPX_NL_HAS_S {int(self.has_s)}",
+            f"#define MCPX_NL_SIZE {self.size}",
+            f"#define MCPX_NL_NNZ {self.nnz}",
+            "MCPX_NL_FN void mcpx_nl_init(const double* MCPX_NL_RESTRICT th, double* MCPX_NL_RESTRICT blk) {",
+            "  (void)th;",
+            "  (void)blk;",
+            *init,
+            "}",
+            "MCPX_NL_FN void mcpx_nl_eval(const double* MCPX_NL_RESTRICT th, const double* MCPX_NL_RESTRICT z,",
+            "                             double* MCPX_NL_RESTRICT blk) {",
+            "  (void)th;",
+            "  (void)z;",
+            *ev,
+            "}",
+            "",
+        ])
+
+    # ---- device module ---------------------------------------------------------
+    def hip_source(self) -> str:
+        return "\n".join([
+            "// generated gfx950 module of one nonlinear MCP (mcp_amd/codegen.py)",
+            "#include <hip/hip_runtime.h>",
+            "#define MCPX_NL_FN __device__ __forceinline__",
+            "#define MCPX_NL_RESTRICT __restrict__",
+            self.body,
+            '#include "ipm_nl_kernel.hpp"',
+            "",
+        ])
+
+    def module_path(self) -> str:
+        return os.path.join(GEN_DIR, f"nl_{self.key}.hsaco")
+
+    def build_module(self, verbose: bool = False) -> str:
+        """Compile (or reuse, by content hash) the gfx950 code object; returns its path."""
+        path = self.module_path()
+        if os.path.exists(path):
+            return path
+        os.makedirs(GEN_DIR, exist_ok=True)
+        src = os.path.join(GEN_DIR, f"nl_{self.key}.hip")
+        with open(src, "w") as f:
+            f.write(self.hip_source())
+        tmp_dir = tempfile.mkdtemp(prefix="mcpx_gen_")
+        tmp = os.path.join(tmp_dir, os.path.basename(path))
+        cmd = [HIPCC, "--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
+               "-Wno-unused-function", "-I", CSRC, "-save-temps", "-o", tmp, src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True, cwd=tmp_dir)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on the generated module {src}:\n{r.stderr[-6000:]}")
+        _check_hazards(tmp_dir)
+        os.replace(tmp, path)
+        shutil.rmtree(tmp_dir, ignore_errors=True)
+        return path
+
+
+def _check_hazards(tmp_dir: str) -> None:
+    """The inline-asm hazard check of the main build (mcp_amd/build.py) on the module's ISA."""
+    checker = os.path.join(os.path.dirname(HERE), "tools", "check_dpp_hazards.py")
+    if not os.path.exists(checker):
+        return
+    for asm in glob.glob(os.path.join(tmp_dir, "*gfx950*.s")):
+        r = subprocess.run([sys.executable, checker, asm], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"inline-asm hazard in the generated module:\n{r.stdout[-2000:]}")

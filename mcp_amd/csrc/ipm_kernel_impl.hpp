@@ -580,7 +580,7 @@ __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, 
   for (int c = 0; c < kc; ++c) {
     const int k = 4 * c + lr;
     const bool kin = k < m;
-    const double dk = sD[kin ? k : 0];
+    const double dk = sD[kin ? k : 0];  // D_k⁻¹
     double cur[NT];
 #pragma unroll
     for (int X = 0; X < NT; ++X) cur[X] = nxt[X];
@@ -593,7 +593,7 @@ __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, 
 #pragma unroll
     for (int X = 0; X < NT; ++X) {
       const bool in = kin && 16 * X + lc < n;
-      af[X] = in ? cur[X] / dk : 0.0;  // A_kj / D_k   (j = 16I + p)
+      af[X] = in ? cur[X] * dk : 0.0;  // A_kj · D_k⁻¹   (j = 16I + p)
       bf[X] = in ? cur[X] : 0.0;       // A_ki         (i = 16J + q)
     }
 #pragma unroll
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
     if (__builtin_amdgcn_readfirstlane(args.status[blockIdx.x]) != STATUS_DEFERRED) return;
   }
   __shared__ double zs[64];
-  __shared__ double sD[SCH ? 64 : 1], sT[SCH ? 64 : 1];
+  __shared__ double sD[SCH ? 64 : 1], sT[SCH ? 64 : 1];  // SCHUR: D_k⁻¹, ty_k
   __shared__ double sB[SCH ? 64 : 1];  // rr, restored for the LU fallback
   const int lane = threadIdx.x;
   const int64_t inst = blockIdx.x;
@@ -832,16 +832,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       double a[NMAX];
       double F, Fc, rhs, w = 1.0;
       const bool rh = ln >= n && ln < n + m;
-      double D = 1.0, ryr = 0.0;  // SCHUR: y-block pivot and reduced y right-hand side
+      // SCHUR: reciprocals of the slack pivot w_k and the y-block pivot D_k, and the
+      // reduced y right-hand side.  Two divisions per lane replace the 13 per step a
+      // quotient-per-use form costs (8 of them in the Schur K-loop).
+      double rw = 1.0, Di = 1.0, ryr = 0.0;
       if constexpr (SCH) {
         qp_residuals<8>(th, zs, ln, n, m, eps, s, F, Fc);
         rhs = -F;
         if (rh) {  // eliminate δs_k (pivot w_k) and then δy_k (pivot D_k)
           w = zs[ln] + tol;
-          D = tol + s / w;
-          ryr = (-F) - (Fc / w);
-          sD[ln - n] = D;
-          sT[ln - n] = ryr / D;
+          rw = 1.0 / w;
+          const double D = tol + s * rw;
+          Di = 1.0 / D;
+          ryr = (-F) - (Fc * rw);
+          sD[ln - n] = Di;
+          sT[ln - n] = ryr * Di;
         }
       } else {
         assemble_row<NMAX, FAMILY, RED, (NC > 0)>(th, zs, ln, n, m, eps, tol, s, a, F, Fc, rhs, w);
@@ -915,11 +920,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         const double acc = dot_strided<8, true>(th + n * n + (rh ? ln - n : 0), m, zs, n, ryr);
         // branch-free consumer: under `if (rh)` the compiler sinks all n loads of
         // the dot into that block at once (n more live registers)
-        const double dzy = acc / D;
+        const double dzy = acc * Di;
         dz = rh ? dzy : dz;
       }
       double ds = 0.0;
-      if (RED && rh) ds = fma(-s, dz, -Fc) / w;  // δs_k = (−F_Ck − s_k δy_k) / w_k
+      if (RED && rh) ds = SCH ? fma(-s, dz, -Fc) * rw : fma(-s, dz, -Fc) / w;  // δs_k = (−F_Ck − s_k δy_k) / w_k
       MCPX_STAMP(2);
 
       // ---- fraction-to-the-boundary line search (:93-100, :127-138) -----

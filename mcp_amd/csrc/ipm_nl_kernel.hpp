@@ -1,0 +1,369 @@
+// ipm_nl_kernel.hpp — gfx950 solver kernels of the nonlinear family
+// (MCPX_FAMILY_NONLINEAR): general G(x, y; θ), H(x, y; θ) evaluated by code
+// generated per problem (mcp_amd/codegen.py), the GPU side of the reference's
+// Symbolics-compiled F!/∇F_z! callbacks (src/mcp.jl:82-120).
+//
+// A generated module is one translation unit:
+//     #define MCPX_NL_N / _M / _P / _HAS_S / _SIZE / _NNZ
+//     mcpx_nl_init(th, blk)      θ-only Jacobian entries, once per instance
+//     mcpx_nl_eval(th, z, blk)   G, H and the z-dependent entries, per Newton step
+//     #include "ipm_nl_kernel.hpp"
+// and this header adds the extern "C" kernels mcpx_nl_solve_{reduced,dense,
+// schur} that the problem's size admits, and the record mcpx_nl_meta that
+// mcpx_module_load (mcpx_api.cpp) reads.
+//
+// One 64-lane wave per instance runs the whole ϵ-continuation / Newton loop
+// (src/solver.jl:64-121), as ipm_solve_kernel does for the QP / affine
+// families.  The generated code is straight-line and its values are
+// wave-uniform, so lane 0 alone runs it and stores the blocks (column-major
+// P = ∂G/∂x, Q = ∂G/∂y, R = ∂H/∂x, S = ∂H/∂y, and G, H) into LDS.  The iterate
+// z = [x; y; s], δz and F live in LDS too, so each linear solver has its own
+// lane ↔ row map:
+//   SCHUR   (∂H/∂y ≡ 0) δs, then δy eliminated exactly; lane i < n owns row i
+//           of S = (P + tol·I) − Q D⁻¹ R, D = tol + s/(y + tol)  (n ≤ 64, m ≤ 128);
+//   REDUCED δs eliminated; lanes [0, n+m) own the (n+m)-dim system;
+//   DENSE   lanes [0, n+2m) own the rows of ∇F + tol·I;
+// all three factor with the register LU with partial pivoting of the QP /
+// affine kernels (lu_solve_rows).  Arithmetic follows oracle/ipm_oracle.c
+// (family MCPX_FAMILY_NONLINEAR) op for op, and the oracle runs the same
+// generated text compiled by gcc, so results are bit-identical.
+#pragma once
+
+#include "ipm_kernel_impl.hpp"
+
+#ifndef MCPX_NL_N
+#error "ipm_nl_kernel.hpp closes a generated module: MCPX_NL_* and mcpx_nl_init/eval come first"
+#endif
+
+namespace mcpx {
+namespace nl {
+
+constexpr int n = MCPX_NL_N, m = MCPX_NL_M, N = n + 2 * m;
+constexpr bool HAS_S = MCPX_NL_HAS_S != 0;
+// block offsets in doubles (mcp_amd/codegen.py)
+constexpr int OFF_P = 0, OFF_Q = n * n, OFF_R = n * n + n * m, OFF_G = n * n + 2 * n * m;
+constexpr int OFF_H = OFF_G + n, OFF_S = OFF_H + m;
+constexpr int RM = (m + 63) / 64;  // (y, s) entries per lane: lane l owns k = l, l + 64
+constexpr int RN = (N + 63) / 64;  // z entries per lane
+
+constexpr int imax(int a, int b) { return a > b ? a : b; }
+constexpr int imin(int a, int b) { return a < b ? a : b; }
+constexpr int rows_of(int solver) {
+  return solver == MCPX_LINSOLVE_DENSE ? N : (solver == MCPX_LINSOLVE_REDUCED ? n + m : n);
+}
+
+template <int SOLVER>
+__device__ __forceinline__ void solve(const KernelArgs& args) {
+  constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR, RED = SOLVER == MCPX_LINSOLVE_REDUCED;
+  constexpr int NR = rows_of(SOLVER);                 // rows of the factored system
+  constexpr int NMAX = imax(8, (NR + 7) / 8 * 8);     // register-row width
+  static_assert(NR >= 1 && NR <= 64, "the linear system must fit one wave");
+  static_assert(!SCH || !HAS_S, "SCHUR needs dH/dy = 0");
+  static_assert(SCH || m <= 64, "REDUCED / DENSE hold every constraint in a lane");
+  constexpr int BLK = imax(1, OFF_S + (SCH ? 0 : m * m));  // RED / DENSE read S (a zero block if absent)
+  constexpr int NZ = imax(1, N), MZ = imax(1, m);
+  __shared__ double blk[BLK];
+  __shared__ double zs[NZ], dzs[NZ], Fs[NZ];
+  __shared__ double RDt[SCH ? imax(1, m * n) : 1];  // SCHUR: R_kj·D_k⁻¹ at k·n + j
+  __shared__ double sRw[SCH ? MZ : 1], sDi[SCH ? MZ : 1], sRy[SCH ? MZ : 1], sTy[SCH ? MZ : 1];
+
+  const int lane = threadIdx.x;
+  const int64_t inst = blockIdx.x;
+  const double* __restrict__ th = args.theta + inst * args.theta_ld;
+  const double tol = args.tol;
+  const bool lx = lane < n;
+
+  for (int i = lane; i < BLK; i += 64) blk[i] = 0.0;  // structural zeros, never written again
+  // src/solver.jl:39-41, 64-66: x₀ = 0, y₀ = 1, s₀ = 1 unless warm-started
+  if (lx) zs[lane] = args.x0 ? args.x0[inst * n + lane] : 0.0;
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int k = lane + 64 * r;
+    if (k < m) {
+      zs[n + k] = args.y0 ? args.y0[inst * m + k] : 1.0;
+      zs[n + m + k] = args.s0 ? args.s0[inst * m + k] : 1.0;
+    }
+  }
+  __syncthreads();
+  if (lane == 0) mcpx_nl_init(th, blk);
+
+  double eps = 1.0;                   // :67
+  double kkt = __builtin_huge_val();  // :68
+  int status = 0;                     // :69
+  int outer = 1;                      // :70
+  int newton = 0;
+  while (kkt > tol && eps > tol && outer < args.max_outer) {  // :71
+    int inner = 1;                                             // :72
+    status = 0;                                                // :73
+    while (kkt > eps && inner < args.max_inner) {              // :75
+      // ---- F!, ∇F_z! (:79-81): the generated code, then F = [G; H − s; s⊙y − ϵ] (src/mcp.jl:76-80)
+      __syncthreads();
+      if (lane == 0) mcpx_nl_eval(th, zs, blk);
+      __syncthreads();
+      double aF = 0.0;
+#pragma unroll
+      for (int r = 0; r < RN; ++r) {
+        const int i = lane + 64 * r;
+        if (i < N) {
+          double f;
+          if (i < n) f = blk[OFF_G + i];
+          else if (i < n + m) f = blk[OFF_H + (i - n)] - zs[i + m];  // H_k − s_k
+          else f = zs[i] * zs[i - m] - eps;                          // s_k·y_k − ϵ
+          Fs[i] = f;
+          aF = max_nan(aF, fabs(f));
+        }
+      }
+      // ‖F‖∞ with NaN propagation (:107), taken now, committed after the step
+      const double kkt_step = ballot(aF != aF) ? __builtin_nan("") : wave_max_nonneg(aF);
+      __syncthreads();
+
+      // ---- Newton system (∇F + tol·I) δz = −F (:81-90) ----------------------
+      double dz = 0.0;
+      bool ok;
+      if constexpr (SCH) {
+        // eliminate δs_k (pivot w_k = y_k + tol), then δy_k (pivot D_k = (0 + tol) + s_k / w_k)
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          const int k = lane + 64 * r;
+          if (k < m) {
+            const double rw = 1.0 / (zs[n + k] + tol);
+            const double Di = 1.0 / (tol + zs[n + m + k] * rw);
+            const double ry = (-Fs[n + k]) - (Fs[n + m + k] * rw);
+            sRw[k] = rw;
+            sDi[k] = Di;
+            sRy[k] = ry;
+            sTy[k] = ry * Di;
+            for (int j = 0; j < n; ++j) RDt[k * n + j] = blk[OFF_R + j * m + k] * Di;
+          }
+        }
+        __syncthreads();
+        // row i of S = (P + tol·I) − Q D⁻¹ R and rr_i = −F_Gi − Σ_k Q_ik ty_k, k ascending
+        const int i = lx ? lane : 0;
+        double a[NMAX];
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+          double v = (j < n) ? blk[OFF_P + j * n + i] : 0.0;
+          if (j == lane) v += tol;
+          a[j] = lx ? v : 0.0;
+        }
+        double rhs = lx ? -Fs[i] : 0.0;
+        for (int k = 0; k < m; ++k) {
+          const double q = lx ? -blk[OFF_Q + k * n + i] : 0.0;
+#pragma unroll
+          for (int j = 0; j < n; ++j) a[j] = fma(q, RDt[k * n + j], a[j]);
+          rhs = fma(q, sTy[k], rhs);
+        }
+        ok = lu_solve_rows<NMAX>(a, rhs, opaque(n), lane, dz);
+        if (ok) {
+          if (lx) dzs[lane] = dz;
+          __syncthreads();
+          // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
+#pragma unroll
+          for (int r = 0; r < RM; ++r) {
+            const int k = lane + 64 * r;
+            if (k < m) {
+              double acc = sRy[k];
+              for (int j = 0; j < n; ++j) acc = fma(-blk[OFF_R + j * m + k], dzs[j], acc);
+              const double dy = acc * sDi[k];
+              dzs[n + k] = dy;
+              dzs[n + m + k] = fma(-zs[n + m + k], dy, -Fs[n + m + k]) * sRw[k];
+            }
+          }
+        }
+      } else if constexpr (RED) {
+        // slack block eliminated exactly: lanes [0, n) x-rows, [n, n+m) y-rows
+        const int i = lane;
+        const bool rx = i < n, ry = i >= n && i < n + m;
+        const int kh = ry ? i - n : 0;
+        const double* px = rx ? blk + OFF_P + i : (ry ? blk + OFF_R + kh : blk);
+        const int sx = rx ? n : (ry ? m : 0);
+        const double* py = rx ? blk + OFF_Q + i : (ry ? blk + OFF_S + kh : blk);
+        const int sy = rx ? n : (ry ? m : 0);
+        const double yk = ry ? zs[imin(n + kh, NZ - 1)] : 1.0;
+        const double sk = ry ? zs[imin(n + m + kh, NZ - 1)] : 1.0;
+        const double w = yk + tol;  // pivot of the eliminated δs_k
+        const double d = sk / w;
+        double a[NMAX];
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+          double v = 0.0;
+          if (j < n) v = px[j * sx];
+          else if (j < n + m) v = (rx || HAS_S) ? py[(j - n) * sy] : 0.0;
+          if (!(rx || ry)) v = 0.0;
+          if (j == i) {
+            v += tol;        // src/solver.jl:81 ∇F + tol*I
+            if (ry) v += d;  // + s_k / w_k
+          }
+          a[j] = v;
+        }
+        double rhs = 0.0;
+        if (rx) rhs = -Fs[i];
+        if (ry) rhs = (-Fs[i]) - (Fs[imin(i + m, NZ - 1)] / w);  // −F_H − F_C / w
+        ok = lu_solve_rows<NMAX>(a, rhs, opaque(n + m), lane, dz);
+        if (ok) {
+          if (rx || ry) dzs[i] = dz;
+          if (ry) dzs[i + m] = fma(-sk, dz, -Fs[i + m]) / w;  // δs_k = (−F_Ck − s_k δy_k) / w_k
+        }
+      } else {
+        // full (n+2m)-dim system, lane i owns row i of ∇F + tol·I
+        const int i = lane;
+        const bool rx = i < n, ry = i >= n && i < n + m, rc = i >= n + m && i < N;
+        const int kh = ry ? i - n : 0, kc = rc ? i - n - m : 0;
+        const double* px = rx ? blk + OFF_P + i : (ry ? blk + OFF_R + kh : blk);
+        const int sx = rx ? n : (ry ? m : 0);
+        const double* py = rx ? blk + OFF_Q + i : (ry ? blk + OFF_S + kh : blk);
+        const int sy = rx ? n : (ry ? m : 0);
+        const bool use_y = rx || (ry && HAS_S);
+        const double sk = rc ? zs[imin(i, NZ - 1)] : 0.0;      // s_k
+        const double yk = rc ? zs[imin(i - m, NZ - 1)] : 0.0;  // y_k
+        double a[NMAX];
+#pragma unroll
+        for (int j = 0; j < NMAX; ++j) {
+          double v = 0.0;
+          if (j < n) {
+            v = (rx || ry) ? px[j * sx] : 0.0;
+          } else if (j < n + m) {
+            const int q = j - n;
+            v = use_y ? py[q * sy] : 0.0;
+            if (rc && q == kc) v = sk;  // ∂(s⊙y)/∂y = diag(s)
+          } else if (j < N) {
+            const int q = j - n - m;
+            if (ry && q == kh) v = -1.0;  // ∂(H − s)/∂s = −I
+            if (rc && q == kc) v = yk;    // ∂(s⊙y)/∂s = diag(y)
+          }
+          if (j == i) v += tol;
+          a[j] = v;
+        }
+        const double rhs = (i < N) ? -Fs[imin(i, NZ - 1)] : 0.0;
+        ok = lu_solve_rows<NMAX>(a, rhs, opaque(N), lane, dz);
+        if (ok && i < N) dzs[i] = dz;
+      }
+      if (!ok) {  // the failed linear solve of :84-88
+        status = 1;
+        break;
+      }
+      __syncthreads();
+
+      // ---- fraction-to-the-boundary line search (:93-100, :127-138) -------
+      double yv[RM > 0 ? RM : 1], sv[RM > 0 ? RM : 1], dyv[RM > 0 ? RM : 1], dsv[RM > 0 ? RM : 1];
+      bool own[RM > 0 ? RM : 1];
+#pragma unroll
+      for (int r = 0; r < RM; ++r) {
+        const int k = lane + 64 * r;
+        own[r] = k < m;
+        const int kk = own[r] ? k : 0;
+        yv[r] = zs[n + kk];
+        sv[r] = zs[n + m + kk];
+        dyv[r] = dzs[n + kk];
+        dsv[r] = dzs[n + m + kk];
+      }
+      uint64_t vs = 0ull, vy = 0ull;
+      double alpha = 1.0;
+      for (int e = 0; e < args.n_trials; ++e) {
+        bool bs = false, by = false;
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          if (own[r]) {
+            bs = bs || (sv[r] + alpha * dsv[r] < args.c_tau * sv[r]);
+            by = by || (yv[r] + alpha * dyv[r] < args.c_tau * yv[r]);
+          }
+        }
+        if (ballot(bs)) vs |= 1ull << e;
+        if (ballot(by)) vy |= 1ull << e;
+        alpha *= args.decay;
+      }
+      const int es = (~vs) ? lowest_lane(~vs) : 64;
+      const int ey = (~vy) ? lowest_lane(~vy) : 64;
+      if (es >= args.n_trials || ey >= args.n_trials) {  // α = NaN
+        status = 1;
+        break;
+      }
+      double as = 1.0, ay = 1.0;
+      for (int e = 0; e < es; ++e) as *= args.decay;
+      for (int e = 0; e < ey; ++e) ay *= args.decay;
+      if (args.alpha_trace && newton < args.trace_len && lane == 0) {
+        uint8_t* tr = args.alpha_trace + ((size_t)inst * args.trace_len + newton) * 2;
+        tr[0] = (uint8_t)es;
+        tr[1] = (uint8_t)ey;
+      }
+      // ---- update (:103-105; x moves with α_s) ------------------------------
+      if (lx) zs[lane] = zs[lane] + as * dzs[lane];
+#pragma unroll
+      for (int r = 0; r < RM; ++r) {
+        if (own[r]) {
+          const int k = lane + 64 * r;
+          zs[n + m + k] = sv[r] + as * dsv[r];
+          zs[n + k] = yv[r] + ay * dyv[r];
+        }
+      }
+      kkt = kkt_step;  // :107
+      ++inner;         // :108
+      ++newton;
+    }
+    eps *= (status == 0) ? args.tight[inner] : args.loose[inner];  // :111-113
+    ++outer;                                                        // :114
+  }
+  if (outer == args.max_outer) status = 1;  // :117-119
+
+  // ---- outputs (:121) -------------------------------------------------------
+  __syncthreads();
+  if (lx) args.x[inst * n + lane] = zs[lane];
+#pragma unroll
+  for (int r = 0; r < RM; ++r) {
+    const int k = lane + 64 * r;
+    if (k < m) {
+      args.y[inst * m + k] = zs[n + k];
+      args.s[inst * m + k] = zs[n + m + k];
+    }
+  }
+  if (args.active_mask && m <= 64) {
+    bool act = false;
+    if (lane < m) act = zs[n + imin(lane, MZ - 1)] > zs[n + m + imin(lane, MZ - 1)];
+    const uint64_t bits = ballot(act);
+    if (lane == 0) args.active_mask[inst] = bits;
+  }
+  if (lane == 0) {
+    args.kkt_error[inst] = kkt;
+    args.eps[inst] = eps;
+    args.outer_iters[inst] = outer;
+    args.status[inst] = status;
+    if (args.newton_iters) args.newton_iters[inst] = newton;
+  }
+}
+
+}  // namespace nl
+}  // namespace mcpx
+
+#define MCPX_NL_CAN_REDUCED (MCPX_NL_N + MCPX_NL_M >= 1 && MCPX_NL_N + MCPX_NL_M <= 64)
+#define MCPX_NL_CAN_DENSE (MCPX_NL_N + 2 * MCPX_NL_M >= 1 && MCPX_NL_N + 2 * MCPX_NL_M <= 64)
+#define MCPX_NL_SCHUR_LDS                                                                             \
+  (8 * (MCPX_NL_N * MCPX_NL_N + 2 * MCPX_NL_N * MCPX_NL_M + MCPX_NL_N + MCPX_NL_M +                   \
+        MCPX_NL_M * MCPX_NL_N + 3 * (MCPX_NL_N + 2 * MCPX_NL_M) + 4 * MCPX_NL_M))
+#define MCPX_NL_CAN_SCHUR                                                                             \
+  (!MCPX_NL_HAS_S && MCPX_NL_N >= 1 && MCPX_NL_N <= 64 && MCPX_NL_M <= 128 &&                         \
+   MCPX_NL_SCHUR_LDS <= 160 * 1024 - 2048)
+
+// mcpx_nl_meta: {layout version, n, m, p, has_s, kernel mask (bit MCPX_LINSOLVE_*), block size, nnz}
+extern "C" {
+__device__ int32_t mcpx_nl_meta[8] = {
+    1, MCPX_NL_N, MCPX_NL_M, MCPX_NL_P, MCPX_NL_HAS_S,
+    (MCPX_NL_CAN_REDUCED << MCPX_LINSOLVE_REDUCED) | (MCPX_NL_CAN_DENSE << MCPX_LINSOLVE_DENSE) |
+        (MCPX_NL_CAN_SCHUR << MCPX_LINSOLVE_SCHUR),
+    MCPX_NL_SIZE, MCPX_NL_NNZ};
+
+#if MCPX_NL_CAN_REDUCED
+__global__ __launch_bounds__(64) void mcpx_nl_solve_reduced(const mcpx::KernelArgs args) {
+  mcpx::nl::solve<MCPX_LINSOLVE_REDUCED>(args);
+}
+#endif
+#if MCPX_NL_CAN_DENSE
+__global__ __launch_bounds__(64) void mcpx_nl_solve_dense(const mcpx::KernelArgs args) {
+  mcpx::nl::solve<MCPX_LINSOLVE_DENSE>(args);
+}
+#endif
+#if MCPX_NL_CAN_SCHUR
+__global__ __launch_bounds__(64) void mcpx_nl_solve_schur(const mcpx::KernelArgs args) {
+  mcpx::nl::solve<MCPX_LINSOLVE_SCHUR>(args);
+}
+#endif
+}  // extern "C"

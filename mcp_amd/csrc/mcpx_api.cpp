@@ -14,6 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -21,6 +24,15 @@
 #include "../../include/mcpx.h"
 #include "ipm_kernel.h"
 #include "sens_kernel.h"
+
+// A generated nonlinear module (MCPX_FAMILY_NONLINEAR, include/mcpx.h): the
+// code object image, its metadata record and the per-device loaded modules.
+struct mcpx_module {
+  std::vector<char> image;
+  int32_t meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // mcpx_nl_meta of csrc/ipm_nl_kernel.hpp
+  std::mutex mu;
+  std::map<int, hipModule_t> loaded;  // device → module, loaded on first use
+};
 
 namespace {
 
@@ -66,9 +78,23 @@ int pick_nmax(int N) {
 }
 
 // Validates desc/params and fills the scalar part + tables of the kernel args.
-int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* nmax) {
+int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* nmax,
+            const mcpx_module* mod = nullptr) {
   if (!d || !p) return fail(MCPX_EINVAL, "desc and params must be non-NULL");
-  const int64_t pd = mcpx_theta_dim(d->family, d->n, d->m);
+  int64_t pd;
+  if (mod) {  // a generated nonlinear module: θ dimension and sizes from its metadata
+    if (d->family != MCPX_FAMILY_NONLINEAR)
+      return fail(MCPX_EINVAL, "a generated module solves family MCPX_FAMILY_NONLINEAR (got %d)", d->family);
+    if (d->n != mod->meta[1] || d->m != mod->meta[2])
+      return fail(MCPX_EINVAL, "desc (n=%d, m=%d) does not match the module (n=%d, m=%d)", d->n, d->m,
+                  mod->meta[1], mod->meta[2]);
+    pd = mod->meta[3];
+  } else {
+    if (d->family == MCPX_FAMILY_NONLINEAR)
+      return fail(MCPX_EINVAL, "family MCPX_FAMILY_NONLINEAR runs through its generated module "
+                  "(mcpx_solve_batch_module*)");
+    pd = mcpx_theta_dim(d->family, d->n, d->m);
+  }
   if (pd < 0) return fail(MCPX_EINVAL, "bad family %d or negative dimensions (n=%d, m=%d)", d->family, d->n, d->m);
   if (d->n + d->m < 1) return fail(MCPX_EINVAL, "empty problem (n = m = 0)");
   if (d->batch < 0) return fail(MCPX_EINVAL, "negative batch");
@@ -76,15 +102,22 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   const int ls = p->linear_solver;
   if (ls != MCPX_LINSOLVE_REDUCED && ls != MCPX_LINSOLVE_DENSE && ls != MCPX_LINSOLVE_SCHUR)
     return fail(MCPX_EINVAL, "unknown linear_solver %d", ls);
-  if (ls == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP)
-    return fail(MCPX_EINVAL, "linear_solver=schur needs the QP family (dH/dy = 0)");
-  const int N = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : (ls == MCPX_LINSOLVE_REDUCED ? d->n + d->m : d->n);
-  const int lanes = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : d->n + d->m;  // one wave: one lane per row
-  *nmax = pick_nmax(N);
-  if (*nmax < 0 || lanes > MCPX_MAX_KKT_DIM)
-    return fail(MCPX_EUNSUPPORTED, "problem size n=%d m=%d exceeds the register-resident kernel for this "
-                "linear_solver (reduced/schur: n+m <= %d, dense: n+2m <= %d)", d->n, d->m, MCPX_MAX_KKT_DIM,
-                MCPX_MAX_KKT_DIM);
+  if (mod) {
+    if (!((mod->meta[5] >> ls) & 1))
+      return fail(MCPX_EUNSUPPORTED, "the generated module has no kernel for linear_solver=%d (n=%d m=%d; schur: "
+                  "dH/dy = 0, n <= 64, m <= 128; reduced: n+m <= 64; dense: n+2m <= 64)", ls, d->n, d->m);
+    *nmax = 0;
+  } else {
+    if (ls == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP)
+      return fail(MCPX_EINVAL, "linear_solver=schur needs the QP family (dH/dy = 0)");
+    const int N = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : (ls == MCPX_LINSOLVE_REDUCED ? d->n + d->m : d->n);
+    const int lanes = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : d->n + d->m;  // one wave: one lane per row
+    *nmax = pick_nmax(N);
+    if (*nmax < 0 || lanes > MCPX_MAX_KKT_DIM)
+      return fail(MCPX_EUNSUPPORTED, "problem size n=%d m=%d exceeds the register-resident kernel for this "
+                  "linear_solver (reduced/schur: n+m <= %d, dense: n+2m <= %d)", d->n, d->m, MCPX_MAX_KKT_DIM,
+                  MCPX_MAX_KKT_DIM);
+  }
   if (!(p->tol > 0) || !(p->min_stepsize > 0) || !(p->decay > 0 && p->decay < 1) || std::isnan(p->tau) ||
       std::isnan(p->tightening_rate) || std::isnan(p->loosening_rate) || p->max_inner_iters < 1 ||
       p->max_outer_iters < 1)
@@ -119,6 +152,35 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   return MCPX_OK;
 }
 
+// ---- generated nonlinear modules ---------------------------------------------
+constexpr int32_t kNLLayout = 1;  // mcpx_nl_meta[0] of csrc/ipm_nl_kernel.hpp
+const char* const kNLKernel[3] = {"mcpx_nl_solve_reduced", "mcpx_nl_solve_dense", "mcpx_nl_solve_schur"};
+
+// `mod` on device `dev` (the current device), loaded on first use.
+int module_on(mcpx_module* mod, int dev, hipModule_t* hm) {
+  std::lock_guard<std::mutex> lock(mod->mu);
+  auto it = mod->loaded.find(dev);
+  if (it != mod->loaded.end()) {
+    *hm = it->second;
+    return MCPX_OK;
+  }
+  HIP_TRY(hipModuleLoadData(hm, mod->image.data()));
+  mod->loaded[dev] = *hm;
+  return MCPX_OK;
+}
+
+// The module's kernel for linear solver `solver` on the current device.
+int nl_function(mcpx_module* mod, int solver, hipFunction_t* f) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  hipModule_t hm;
+  const int rc = module_on(mod, dev, &hm);
+  if (rc) return rc;
+  if (hipModuleGetFunction(f, hm, kNLKernel[solver]) != hipSuccess)
+    return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel", kNLKernel[solver]);
+  return MCPX_OK;
+}
+
 // Picks the kernel: a compile-time-(n, m) specialisation when one exists (and
 // MCPX_GENERIC_KERNELS is not set), else the runtime-(n, m) kernel for nmax.
 hipError_t launch(int nmax, const mcpx::KernelArgs& a, int64_t nb, hipStream_t st) {
@@ -138,7 +200,13 @@ hipError_t launch(int nmax, const mcpx::KernelArgs& a, int64_t nb, hipStream_t s
 }
 
 int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
-                  const double* s0, const mcpx_out* o, mcpx::KernelArgs a, int nmax, hipStream_t st) {
+                  const double* s0, const mcpx_out* o, mcpx::KernelArgs a, int nmax, hipStream_t st,
+                  mcpx_module* mod = nullptr) {
+  hipFunction_t nlf = nullptr;  // generated module: its kernel, launched by hipModuleLaunchKernel
+  if (mod) {
+    const int rc = nl_function(mod, a.solver, &nlf);
+    if (rc) return rc;
+  }
   const int64_t CH = (int64_t)1 << 30;
   const int n = d->n, m = d->m;
   for (int64_t b0 = 0; b0 < d->batch; b0 += CH) {
@@ -158,7 +226,12 @@ int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, con
     a.active_mask = o->active_mask ? o->active_mask + b0 : nullptr;
     a.alpha_trace = (o->alpha_trace && o->trace_len > 0) ? o->alpha_trace + b0 * (int64_t)o->trace_len * 2 : nullptr;
     a.trace_len = o->alpha_trace ? o->trace_len : 0;
-    HIP_TRY(launch(nmax, a, nb, st));
+    if (mod) {
+      void* params[] = {&a};
+      HIP_TRY(hipModuleLaunchKernel(nlf, (unsigned)nb, 1, 1, 64, 1, 1, 0, st, params, nullptr));
+    } else {
+      HIP_TRY(launch(nmax, a, nb, st));
+    }
   }
   return MCPX_OK;
 }
@@ -177,13 +250,14 @@ struct DevBuf {
 
 // One device's share of mcpx_solve_batch: instances [b0, b0+nb).
 int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
-                const double* s0, const mcpx_params* prm, mcpx_out* o, int64_t b0, int64_t nb) {
+                const double* s0, const mcpx_params* prm, mcpx_out* o, int64_t b0, int64_t nb,
+                mcpx_module* mod = nullptr) {
   HIP_TRY(hipSetDevice(dev));
   int rc = check_device(dev);
   if (rc) return rc;
   mcpx::KernelArgs a;
   int nmax;
-  if ((rc = prepare(d, prm, &a, &nmax))) return rc;
+  if ((rc = prepare(d, prm, &a, &nmax, mod))) return rc;
   const int n = d->n, m = d->m;
   if (m > 64 && o->active_mask) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
   DevBuf<double> th, dx0, dy0, ds0, x, y, s, kkt, eps;
@@ -208,7 +282,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   od.active_mask = am.p; od.alpha_trace = tr.p; od.trace_len = want_tr ? o->trace_len : 0;
   mcpx_desc dd = *d;
   dd.batch = nb;
-  if ((rc = launch_chunks(&dd, th.p, dx0.p, dy0.p, ds0.p, &od, a, nmax, nullptr))) return rc;
+  if ((rc = launch_chunks(&dd, th.p, dx0.p, dy0.p, ds0.p, &od, a, nmax, nullptr, mod))) return rc;
   HIP_TRY(hipDeviceSynchronize());
   auto back = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     return bytes ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
@@ -344,6 +418,58 @@ int sens_inputs_ok(const mcpx_desc* d, const double* theta, const double* x, con
   return MCPX_OK;
 }
 
+// mcpx_solve_batch_device / mcpx_solve_batch_module_device (mod = nullptr: QP / affine kernels).
+int solve_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x0,
+                      const double* y0, const double* s0, const mcpx_params* prm, const mcpx_out* o,
+                      void* stream) {
+  mcpx::KernelArgs a;
+  int nmax;
+  int rc = prepare(d, prm, &a, &nmax, mod);
+  if (rc) return rc;
+  if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
+  if (d->batch == 0) return MCPX_OK;
+  if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
+  if (o->active_mask && d->m > 64) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if ((rc = check_device(dev))) return rc;
+  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod);
+}
+
+// mcpx_solve_batch / mcpx_solve_batch_module: contiguous shards, one host thread per device.
+int solve_host_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x0,
+                    const double* y0, const double* s0, const mcpx_params* prm, int num_devices,
+                    mcpx_out* o) {
+  mcpx::KernelArgs a;
+  int nmax;
+  int rc = prepare(d, prm, &a, &nmax, mod);
+  if (rc) return rc;
+  if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
+  if (d->batch == 0) return MCPX_OK;
+  if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
+  const int avail = mcpx_device_count();
+  if (avail < 1) return fail(MCPX_ENODEV, "no HIP device visible");
+  if (num_devices <= 0 || num_devices > avail) num_devices = avail;
+  if ((int64_t)num_devices > d->batch) num_devices = (int)d->batch;
+  // contiguous shards: device g gets ⌊B/G⌋ (+1 for g < B mod G)
+  std::vector<int64_t> start(num_devices + 1, 0);
+  for (int g = 0; g < num_devices; ++g)
+    start[g + 1] = start[g] + d->batch / num_devices + (g < d->batch % num_devices ? 1 : 0);
+  if (num_devices == 1) return solve_shard(0, d, theta, x0, y0, s0, prm, o, 0, d->batch, mod);
+  std::vector<int> rcs(num_devices, 0);
+  std::vector<std::string> errs(num_devices);
+  std::vector<std::thread> th;
+  for (int g = 0; g < num_devices; ++g)
+    th.emplace_back([&, g] {
+      rcs[g] = solve_shard(g, d, theta, x0, y0, s0, prm, o, start[g], start[g + 1] - start[g], mod);
+      if (rcs[g]) errs[g] = g_err;
+    });
+  for (auto& t : th) t.join();
+  for (int g = 0; g < num_devices; ++g)
+    if (rcs[g]) return fail(rcs[g], "device %d: %s", g, errs[g].c_str());
+  return MCPX_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -379,50 +505,12 @@ int mcpx_device_count(void) {
 
 int mcpx_solve_batch_device(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                             const double* s0, const mcpx_params* prm, const mcpx_out* o, void* stream) {
-  mcpx::KernelArgs a;
-  int nmax;
-  int rc = prepare(d, prm, &a, &nmax);
-  if (rc) return rc;
-  if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
-  if (d->batch == 0) return MCPX_OK;
-  if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
-  if (o->active_mask && d->m > 64) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if ((rc = check_device(dev))) return rc;
-  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream);
+  return solve_device_impl(nullptr, d, theta, x0, y0, s0, prm, o, stream);
 }
 
 int mcpx_solve_batch(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                      const double* s0, const mcpx_params* prm, int num_devices, mcpx_out* o) {
-  mcpx::KernelArgs a;
-  int nmax;
-  int rc = prepare(d, prm, &a, &nmax);
-  if (rc) return rc;
-  if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
-  if (d->batch == 0) return MCPX_OK;
-  if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
-  const int avail = mcpx_device_count();
-  if (avail < 1) return fail(MCPX_ENODEV, "no HIP device visible");
-  if (num_devices <= 0 || num_devices > avail) num_devices = avail;
-  if ((int64_t)num_devices > d->batch) num_devices = (int)d->batch;
-  // contiguous shards: device g gets ⌊B/G⌋ (+1 for g < B mod G)
-  std::vector<int64_t> start(num_devices + 1, 0);
-  for (int g = 0; g < num_devices; ++g)
-    start[g + 1] = start[g] + d->batch / num_devices + (g < d->batch % num_devices ? 1 : 0);
-  if (num_devices == 1) return solve_shard(0, d, theta, x0, y0, s0, prm, o, 0, d->batch);
-  std::vector<int> rcs(num_devices, 0);
-  std::vector<std::string> errs(num_devices);
-  std::vector<std::thread> th;
-  for (int g = 0; g < num_devices; ++g)
-    th.emplace_back([&, g] {
-      rcs[g] = solve_shard(g, d, theta, x0, y0, s0, prm, o, start[g], start[g + 1] - start[g]);
-      if (rcs[g]) errs[g] = g_err;
-    });
-  for (auto& t : th) t.join();
-  for (int g = 0; g < num_devices; ++g)
-    if (rcs[g]) return fail(rcs[g], "device %d: %s", g, errs[g].c_str());
-  return MCPX_OK;
+  return solve_host_impl(nullptr, d, theta, x0, y0, s0, prm, num_devices, o);
 }
 
 int mcpx_vjp_batch_device(const mcpx_desc* d, const double* theta, const double* x, const double* y,
@@ -481,6 +569,78 @@ int mcpx_jvp_batch(const mcpx_desc* d, const double* theta, const double* x, con
   if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
   return sens_host(true, d, a, nmax, theta, x, y, s, nullptr, nullptr, nullptr, theta_dot, num_devices, zdot,
                    status);
+}
+
+// ---- generated nonlinear modules (MCPX_FAMILY_NONLINEAR) ----------------------
+
+int mcpx_solve_batch_module(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x0,
+                            const double* y0, const double* s0, const mcpx_params* prm, int num_devices,
+                            mcpx_out* o) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  return solve_host_impl(mod, d, theta, x0, y0, s0, prm, num_devices, o);
+}
+
+int mcpx_solve_batch_module_device(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x0,
+                                   const double* y0, const double* s0, const mcpx_params* prm,
+                                   const mcpx_out* o, void* stream) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  return solve_device_impl(mod, d, theta, x0, y0, s0, prm, o, stream);
+}
+
+int mcpx_module_load(const char* path, mcpx_module** out) {
+  if (!path || !out) return fail(MCPX_EINVAL, "path and out must be non-NULL");
+  *out = nullptr;
+  std::vector<char> img;
+  {
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(MCPX_EINVAL, "cannot open code object '%s'", path);
+    char buf[1 << 16];
+    size_t k;
+    while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) img.insert(img.end(), buf, buf + k);
+    std::fclose(f);
+  }
+  if (img.empty()) return fail(MCPX_EINVAL, "code object '%s' is empty", path);
+  if (mcpx_device_count() < 1) return fail(MCPX_ENODEV, "no HIP device visible");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  int rc = check_device(dev);
+  if (rc) return rc;
+  std::unique_ptr<mcpx_module> mod(new mcpx_module);
+  mod->image = std::move(img);
+  hipModule_t hm;
+  if ((rc = module_on(mod.get(), dev, &hm))) return rc;
+  hipDeviceptr_t dp = nullptr;
+  size_t bytes = 0;
+  if (hipModuleGetGlobal(&dp, &bytes, hm, "mcpx_nl_meta") != hipSuccess || bytes != sizeof mod->meta) {
+    (void)hipModuleUnload(hm);
+    return fail(MCPX_EINVAL, "'%s' is not an mcpx nonlinear module (no mcpx_nl_meta)", path);
+  }
+  HIP_TRY(hipMemcpyDtoH(mod->meta, dp, bytes));
+  if (mod->meta[0] != kNLLayout) {
+    (void)hipModuleUnload(hm);
+    return fail(MCPX_EINVAL, "module layout version %d, this library expects %d", mod->meta[0], kNLLayout);
+  }
+  *out = mod.release();
+  return MCPX_OK;
+}
+
+int mcpx_module_dims(const mcpx_module* mod, int32_t* n, int32_t* m, int32_t* p, int32_t* solvers) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  if (n) *n = mod->meta[1];
+  if (m) *m = mod->meta[2];
+  if (p) *p = mod->meta[3];
+  if (solvers) *solvers = mod->meta[5];
+  return MCPX_OK;
+}
+
+void mcpx_module_unload(mcpx_module* mod) {
+  if (!mod) return;
+  int prev = 0;
+  const bool have = hipGetDevice(&prev) == hipSuccess;
+  for (auto& kv : mod->loaded)
+    if (hipSetDevice(kv.first) == hipSuccess) (void)hipModuleUnload(kv.second);
+  if (have) (void)hipSetDevice(prev);
+  delete mod;
 }
 
 }  // extern "C"

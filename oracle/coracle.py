@@ -22,7 +22,9 @@ _lib = None
 
 def build(force: bool = False) -> str:
     """Compile the oracle with oracle/Makefile (gcc)."""
-    if force or not os.path.exists(_LIB_PATH):
+    if force:
+        subprocess.run(["make", "-s", "-B", "-C", _HERE], check=True)
+    else:  # incremental: rebuilds when ipm_oracle.c / mcpx.h are newer than the library
         subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return _LIB_PATH
 
@@ -73,6 +75,80 @@ def solve_batch(family: int, n: int, m: int, theta: np.ndarray, *, x0=None, y0=N
                                   C.byref(prm), C.byref(out), int(nthreads))
     if rc != 0:
         raise ValueError(f"oracle_solve_batch failed with code {rc}")
+    return r
+
+
+class OracleNL(C.Structure):
+    """oracle_nl of ipm_oracle.c: the generated init/eval of one nonlinear MCP."""
+
+    _fields_ = [("init", C.c_void_p), ("eval", C.c_void_p), ("p", C.c_int32), ("has_s", C.c_int32),
+                ("size", C.c_int32), ("pad_", C.c_int32)]
+
+
+_GEN_DIR = os.path.join(_HERE, "_build", "gen")
+_nl_libs: dict = {}
+
+
+def nl_lib(nl):
+    """gcc-compile the SAME generated text the gfx950 module is built from
+    (mcp_amd/codegen.py NLSystem.body) into oracle/_build/gen/nl_<key>.so."""
+    if nl.key in _nl_libs:
+        return _nl_libs[nl.key]
+    os.makedirs(_GEN_DIR, exist_ok=True)
+    so = os.path.join(_GEN_DIR, f"nl_{nl.key}.so")
+    if not os.path.exists(so):
+        src = os.path.join(_GEN_DIR, f"nl_{nl.key}.c")
+        with open(src, "w") as f:
+            f.write("#include <math.h>\n#define MCPX_NL_FN static inline\n#define MCPX_NL_RESTRICT restrict\n")
+            f.write(nl.body)
+            f.write("\nvoid oracle_nl_init(const double* th, double* blk) { mcpx_nl_init(th, blk); }\n"
+                    "void oracle_nl_eval(const double* th, const double* z, double* blk) "
+                    "{ mcpx_nl_eval(th, z, blk); }\n")
+        tmp = f"{so}.{os.getpid()}.tmp"
+        subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
+                        "-o", tmp, src, "-lm"], check=True)
+        os.replace(tmp, so)
+    L = C.CDLL(so)
+    _nl_libs[nl.key] = L
+    return L
+
+
+def solve_batch_nl(nl, theta: np.ndarray, *, x0=None, y0=None, s0=None, params: Params | None = None,
+                   trace_len: int = 0, nthreads: int = 1, **kw) -> dict:
+    """Oracle of mcpx_solve_batch_module: nl is the problem's codegen.NLSystem."""
+    from mcp_amd._abi import FAMILY_NONLINEAR
+
+    theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+    B, ld = theta.shape
+    n, m = nl.n, nl.m
+    if ld < nl.p:
+        raise ValueError(f"theta has {ld} columns, the problem needs {nl.p}")
+    prm = params if params is not None else make_params(**kw)
+    conv = lambda a, k: None if a is None else np.ascontiguousarray(np.broadcast_to(a, (B, k)), dtype=np.float64)
+    x0, y0, s0 = conv(x0, n), conv(y0, m), conv(s0, m)
+    words = max(1, (m + 63) // 64)
+    r = dict(
+        x=np.empty((B, n)), y=np.empty((B, m)), s=np.empty((B, m)), kkt_error=np.empty(B),
+        eps=np.empty(B), outer_iters=np.empty(B, np.int32), status=np.empty(B, np.int32),
+        newton_iters=np.empty(B, np.int32), active_mask=np.empty((B, words), np.uint64),
+        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+    )
+    out = Out(_ptr(r["x"]), _ptr(r["y"]), _ptr(r["s"]), _ptr(r["kkt_error"]), _ptr(r["eps"]),
+              _ptr(r["outer_iters"]), _ptr(r["status"]), _ptr(r["newton_iters"]),
+              _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
+              int(trace_len), 0)
+    G = nl_lib(nl)
+    spec = OracleNL(C.cast(G.oracle_nl_init, C.c_void_p).value, C.cast(G.oracle_nl_eval, C.c_void_p).value,
+                    nl.p, int(nl.has_s), nl.size, 0)
+    L = lib()
+    L.oracle_solve_batch_nl.restype = C.c_int
+    L.oracle_solve_batch_nl.argtypes = [C.POINTER(Desc), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.POINTER(Params), C.POINTER(Out), C.c_int, C.POINTER(OracleNL)]
+    desc = Desc(FAMILY_NONLINEAR, n, m, 0, B, ld)
+    rc = L.oracle_solve_batch_nl(C.byref(desc), _ptr(theta), _ptr(x0), _ptr(y0), _ptr(s0), C.byref(prm),
+                                 C.byref(out), int(nthreads), C.byref(spec))
+    if rc != 0:
+        raise ValueError(f"oracle_solve_batch_nl failed with code {rc}")
     return r
 
 

@@ -33,13 +33,14 @@
  *    d_k = s_k / w_k added to the (H_k, y_k) diagonal entry after its tol,
  *    rhs_Hk = (−F_Hk) − (F_Ck / w_k); the (n+m) system is solved by the LU
  *    above and δs_k = fma(−s_k, δy_k, −F_Ck) / w_k;
- *  - linear_solver = MCPX_LINSOLVE_SCHUR (QP family) also eliminates the
- *    diagonal y block D_k = (0 + tol) + d_k: ry_k = (−F_Hk) − (F_Ck / w_k),
- *    ty_k = ry_k / D_k; S_ij = fma chain over k = 0 .. 4⌈m/4⌉−1 starting at
- *    (M_ij + tol·[i=j]) of A_ki · (A_kj / D_k) (k ≥ m contributes fma(0, 0, ·),
+ *  - linear_solver = MCPX_LINSOLVE_SCHUR (QP family) works with reciprocals:
+ *    r_k = 1 / w_k, D_k = (0 + tol) + s_k·r_k, Dⁱ_k = 1 / D_k,
+ *    ry_k = (−F_Hk) − (F_Ck·r_k), ty_k = ry_k·Dⁱ_k; S_ij = fma chain over
+ *    k = 0 .. 4⌈m/4⌉−1 starting at (M_ij + tol·[i=j]) of A_ki · (A_kj·Dⁱ_k)
+ *    (k ≥ m contributes fma(0, 0, ·),
  *    the zero padding of the fp64 MFMA K-chunks); rr_i = fma chain over k of
  *    A_ki · ty_k starting at −F_Gi; δx = S \ rr; δy_k = (fma chain over j
- *    of −A_kj · δx_j starting at ry_k) / D_k; δs as above.  S \ rr: when M is
+ *    of −A_kj · δx_j starting at ry_k)·Dⁱ_k; δs_k = fma(−s_k, δy_k, −F_Ck)·r_k.  S \ rr: when M is
  *    exactly symmetric (checked once per instance), S is symmetric and — if
  *    every pivot of elimination without pivoting is > 0 — positive definite,
  *    so it is solved by pivot-free Gauss-Jordan elimination (gj_spd_solve:
@@ -54,7 +55,13 @@
  *    rounding only);
  *  - line search α = decayᵉ by repeated multiplication, predicate
  *    v + α·δ < (1−τ)·v evaluated without contraction (src/solver.jl:127-138);
- *  - ϵ factors 1 − exp(−t·k) / 1 + exp(−l·k) from libm (src/solver.jl:111-113).
+ *  - ϵ factors 1 − exp(−t·k) / 1 + exp(−l·k) from libm (src/solver.jl:111-113);
+ *  - family MCPX_FAMILY_NONLINEAR: the per-step Jacobian blocks and G, H come
+ *    from the problem's generated code (oracle_nl.init / .eval — the text of
+ *    mcp_amd/codegen.py compiled by gcc, oracle/nl.py); rows are read from
+ *    them as the affine family reads θ (G rows: P, Q and g = G(z) itself; H
+ *    rows: R, S and h − s); SCHUR (∂H/∂y ≡ 0) without the QP family's K
+ *    padding and SPD attempt.
  * Build with -ffp-contract=off (oracle/Makefile) so that only the explicit
  * fma() calls fuse.
  */
@@ -73,6 +80,21 @@ typedef struct oracle_tables {
   double tight[MCPX_MAX_INNER_ITERS + 1];
   double loose[MCPX_MAX_INNER_ITERS + 1];
 } oracle_tables;
+
+/* MCPX_FAMILY_NONLINEAR: the generated evaluation code of one problem.  `blk`
+ * holds the blocks P, Q, R, g, h, S of mcp_amd/codegen.py's layout; init
+ * writes the θ-only Jacobian entries once per instance, eval G, H and the
+ * z-dependent entries at z = [x; y]. */
+typedef struct oracle_nl {
+  void (*init)(const double* th, double* blk);
+  void (*eval)(const double* th, const double* z, double* blk);
+  int32_t p, has_s, size, pad_;
+} oracle_nl;
+
+/* doubles of the block array, the S block always included (zero when absent) */
+static size_t nl_blk_doubles(int n, int m) {
+  return (size_t)n * n + 2 * (size_t)n * m + n + m + (size_t)m * m;
+}
 
 /* Validates the keyword arguments and precomputes what the reference computes
  * inline.  Returns 0 or MCPX_EINVAL / MCPX_EUNSUPPORTED. */
@@ -131,6 +153,13 @@ static double family_row(int family, int n, int m, const double* th, const doubl
         acc = fma(row[n + k], y[k], acc);
       }
       return acc - phi[i];
+    } else if (family == MCPX_FAMILY_NONLINEAR) {
+      /* generated blocks (mcp_amd/codegen.py): P = ∂G/∂x, Q = ∂G/∂y, g = G(x, y; θ) */
+      const double* P = th;
+      const double* Q = th + (size_t)n * n;
+      for (int j = 0; j < n; ++j) row[j] = P[(size_t)j * n + i];
+      for (int k = 0; k < m; ++k) row[n + k] = Q[(size_t)k * n + i];
+      return th[(size_t)n * n + 2 * (size_t)n * m + i];
     } else { /* G = P x + Q y + g */
       const double* P = th;
       const double* Q = th + (size_t)n * n;
@@ -157,6 +186,13 @@ static double family_row(int family, int n, int m, const double* th, const doubl
         acc = fma(row[j], x[j], acc);
       }
       return (acc - b[k]) - s[k];
+    } else if (family == MCPX_FAMILY_NONLINEAR) {
+      /* R = ∂H/∂x, S = ∂H/∂y (a zero block when H does not depend on y), h = H(x, y; θ) */
+      const double* R = th + (size_t)n * n + (size_t)n * m;
+      const double* S = th + (size_t)n * n + 2 * (size_t)n * m + n + m;
+      for (int j = 0; j < n; ++j) row[j] = R[(size_t)j * m + k];
+      for (int q = 0; q < m; ++q) row[n + q] = S[(size_t)q * m + k];
+      return th[(size_t)n * n + 2 * (size_t)n * m + n + k] - s[k];
     } else {
       const double* R = th + (size_t)n * n + (size_t)n * m;
       const double* S = th + (size_t)n * n + 2 * (size_t)n * m;
@@ -259,11 +295,13 @@ static int linesearch_exponent(const double* v, const double* d, int cnt, const 
 }
 
 typedef struct ws {
-  double *J, *Jr, *Js, *bs, *row, *F, *b, *dz, *z, *sD, *sry, *sty;
+  double *J, *Jr, *Js, *bs, *row, *F, *b, *dz, *z, *sD, *srw, *sry, *sty;
+  double* blk; /* MCPX_FAMILY_NONLINEAR: the generated blocks */
   int *remaining, *step_of, *prow;
 } ws;
 
 static int ws_alloc(ws* w, int N) {
+  w->blk = NULL;
   w->J = (double*)malloc(sizeof(double) * (size_t)N * N);
   w->Jr = (double*)malloc(sizeof(double) * (size_t)N * N);
   w->Js = (double*)malloc(sizeof(double) * (size_t)N * N);
@@ -271,6 +309,7 @@ static int ws_alloc(ws* w, int N) {
   w->row = (double*)malloc(sizeof(double) * N);
   w->sD = (double*)malloc(sizeof(double) * N);
   w->sry = (double*)malloc(sizeof(double) * N);
+  w->srw = (double*)malloc(sizeof(double) * N);
   w->sty = (double*)malloc(sizeof(double) * N);
   w->F = (double*)malloc(sizeof(double) * N);
   w->b = (double*)malloc(sizeof(double) * N);
@@ -279,17 +318,18 @@ static int ws_alloc(ws* w, int N) {
   w->remaining = (int*)malloc(sizeof(int) * N);
   w->step_of = (int*)malloc(sizeof(int) * N);
   w->prow = (int*)malloc(sizeof(int) * N);
-  return (w->J && w->Jr && w->Js && w->bs && w->sD && w->sry && w->sty && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
+  return (w->J && w->Jr && w->Js && w->bs && w->sD && w->srw && w->sry && w->sty && w->row && w->F && w->b && w->dz && w->z && w->remaining && w->step_of && w->prow) ? 0 : -1;
 }
 static void ws_free(ws* w) {
-  free(w->J); free(w->Jr); free(w->Js); free(w->bs); free(w->sD); free(w->sry); free(w->sty); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
+  free(w->J); free(w->Jr); free(w->Js); free(w->bs); free(w->sD); free(w->srw); free(w->sry); free(w->sty); free(w->row); free(w->F); free(w->b); free(w->dz); free(w->z);
   free(w->remaining); free(w->step_of); free(w->prow);
+  free(w->blk);
 }
 
 /* One instance: src/solver.jl:35-122. */
 static void solve_one(const mcpx_desc* d, const double* th, const double* x0, const double* y0,
                       const double* s0, const mcpx_params* p, const oracle_tables* t, ws* w,
-                      int64_t inst, const mcpx_out* o) {
+                      int64_t inst, const mcpx_out* o, const oracle_nl* nl) {
   const int n = d->n, m = d->m, N = n + 2 * m;
   double* z = w->z;
   /* src/solver.jl:39-41,64-66 */
@@ -302,7 +342,14 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
   int outer = 1;              /* :70 */
   int newton = 0;
   int m_sym = 0; /* SCHUR: M exactly symmetric → try the SPD Gauss-Jordan first */
-  if (p->linear_solver == MCPX_LINSOLVE_SCHUR) {
+  /* MCPX_FAMILY_NONLINEAR: family_row reads the generated blocks instead of θ */
+  const double* fth = th;
+  if (nl) {
+    memset(w->blk, 0, sizeof(double) * nl_blk_doubles(n, m));
+    nl->init(th, w->blk);
+    fth = w->blk;
+  }
+  if (p->linear_solver == MCPX_LINSOLVE_SCHUR && d->family == MCPX_FAMILY_QP) {
     m_sym = 1;
     for (int i = 0; i < n && m_sym; ++i)
       for (int j = 0; j < n; ++j)
@@ -313,8 +360,9 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
     status = MCPX_STATUS_SOLVED; /* :73 */
     while (kkt > eps && inner < p->max_inner_iters) { /* :75 */
       /* :79-82 F!, ∇F_z!, A = ∇F + tol I, b = −F */
+      if (nl) nl->eval(th, z, w->blk);
       for (int i = 0; i < N; ++i) {
-        w->F[i] = family_row(d->family, n, m, th, z, eps, i, w->J + (size_t)i * N);
+        w->F[i] = family_row(d->family, n, m, fth, z, eps, i, w->J + (size_t)i * N);
         w->J[(size_t)i * N + i] += p->tol;
         w->b[i] = -w->F[i];
       }
@@ -326,15 +374,17 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
         }
       } else if (p->linear_solver == MCPX_LINSOLVE_SCHUR) {
         /* slack block, then the diagonal y block: n×n Schur complement (QP family) */
-        const int m4 = (m + 3) / 4 * 4;
+        const int m4 = d->family == MCPX_FAMILY_QP ? (m + 3) / 4 * 4 : m; /* QP: the MFMA's K padding */
         for (int k = 0; k < m; ++k) {
           const int h = n + k, c = n + m + k;
-          const double wk = w->J[(size_t)c * N + c];  /* y_k + tol */
-          const double D = w->J[(size_t)h * N + h] + z[c] / wk;
-          const double ry = w->b[h] - (w->F[c] / wk);
-          w->sD[k] = D;
+          const double rwk = 1.0 / w->J[(size_t)c * N + c];  /* 1 / (y_k + tol) */
+          const double D = w->J[(size_t)h * N + h] + z[c] * rwk;
+          const double Di = 1.0 / D;
+          const double ry = w->b[h] - (w->F[c] * rwk);
+          w->sD[k] = Di;   /* D_k⁻¹ */
+          w->srw[k] = rwk;
           w->sry[k] = ry;
-          w->sty[k] = ry / D;
+          w->sty[k] = ry * Di;
         }
         for (int i = 0; i < n; ++i)
           for (int j = 0; j < n; ++j) {
@@ -343,7 +393,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
               if (k < m) {
                 const double aki = -w->J[(size_t)i * N + n + k]; /* A_ki */
                 const double akj = w->J[(size_t)(n + k) * N + j];  /* A_kj */
-                acc = fma(aki, akj / w->sD[k], acc);
+                acc = fma(aki, akj * w->sD[k], acc);
               } else {
                 acc = fma(0.0, 0.0, acc);
               }
@@ -368,12 +418,11 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
         for (int k = 0; k < m; ++k) {
           double acc = w->sry[k];
           for (int j = 0; j < n; ++j) acc = fma(-w->J[(size_t)(n + k) * N + j], w->dz[j], acc);
-          w->dz[n + k] = acc / w->sD[k];
+          w->dz[n + k] = acc * w->sD[k];
         }
         for (int k = 0; k < m; ++k) {
           const int c = n + m + k;
-          const double wk = w->J[(size_t)c * N + c];
-          w->dz[c] = fma(-z[c], w->dz[n + k], -w->F[c]) / wk;
+          w->dz[c] = fma(-z[c], w->dz[n + k], -w->F[c]) * w->srw[k];
         }
       } else {
         /* exact elimination of the slack block, then LU of the (n+m) Schur complement */
@@ -452,6 +501,7 @@ typedef struct job {
   const mcpx_params* p;
   const oracle_tables* t;
   const mcpx_out* o;
+  const oracle_nl* nl; /* MCPX_FAMILY_NONLINEAR, else NULL */
   int64_t next; /* shared work counter */
   pthread_mutex_t mu;
   int err;
@@ -460,7 +510,12 @@ typedef struct job {
 static void* worker(void* arg) {
   job* j = (job*)arg;
   ws w;
-  if (ws_alloc(&w, j->d->n + 2 * j->d->m)) {
+  int bad = ws_alloc(&w, j->d->n + 2 * j->d->m);
+  if (!bad && j->nl) {
+    w.blk = (double*)malloc(sizeof(double) * (nl_blk_doubles(j->d->n, j->d->m) + 1));
+    bad = w.blk == NULL;
+  }
+  if (bad) {
     pthread_mutex_lock(&j->mu);
     j->err = 1;
     pthread_mutex_unlock(&j->mu);
@@ -472,7 +527,7 @@ static void* worker(void* arg) {
     const int64_t b = j->next++;
     pthread_mutex_unlock(&j->mu);
     if (b >= j->d->batch) break;
-    solve_one(j->d, j->theta + b * j->d->theta_ld, j->x0, j->y0, j->s0, j->p, j->t, &w, b, j->o);
+    solve_one(j->d, j->theta + b * j->d->theta_ld, j->x0, j->y0, j->s0, j->p, j->t, &w, b, j->o, j->nl);
   }
   ws_free(&w);
   return NULL;
@@ -485,22 +540,14 @@ int64_t oracle_theta_dim(int family, int n, int m) {
   return -1;
 }
 
-/* Batched entry: same argument meaning as mcpx_solve_batch (host buffers),
- * instances distributed over `nthreads` POSIX threads (one instance per task). */
-int oracle_solve_batch(const mcpx_desc* d, const double* theta, const double* x0,
-                       const double* y0, const double* s0, const mcpx_params* p,
-                       mcpx_out* o, int nthreads) {
-  if (!d || !theta || !p || !o || !o->x || !o->y || !o->s || !o->kkt_error || !o->eps ||
-      !o->outer_iters || !o->status)
-    return MCPX_EINVAL;
-  const int64_t pd = oracle_theta_dim(d->family, d->n, d->m);
-  if (pd < 0 || d->n + d->m < 1 || d->batch < 0 || d->theta_ld < pd) return MCPX_EINVAL;
-  if (p->linear_solver == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP) return MCPX_EINVAL;
+static int run_batch(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
+                     const double* s0, const mcpx_params* p, mcpx_out* o, int nthreads,
+                     const oracle_nl* nl) {
   oracle_tables t;
   const int rc = oracle_build_tables(p, &t);
   if (rc) return rc;
   job j;
-  j.d = d; j.theta = theta; j.x0 = x0; j.y0 = y0; j.s0 = s0; j.p = p; j.t = &t; j.o = o;
+  j.d = d; j.theta = theta; j.x0 = x0; j.y0 = y0; j.s0 = s0; j.p = p; j.t = &t; j.o = o; j.nl = nl;
   j.next = 0; j.err = 0;
   pthread_mutex_init(&j.mu, NULL);
   if (nthreads < 1) nthreads = 1;
@@ -514,6 +561,33 @@ int oracle_solve_batch(const mcpx_desc* d, const double* theta, const double* x0
   }
   pthread_mutex_destroy(&j.mu);
   return j.err ? MCPX_EINVAL : 0;
+}
+
+static int outputs_ok(const mcpx_out* o) {
+  return o && o->x && o->y && o->s && o->kkt_error && o->eps && o->outer_iters && o->status;
+}
+
+/* Batched entry: same argument meaning as mcpx_solve_batch (host buffers),
+ * instances distributed over `nthreads` POSIX threads (one instance per task). */
+int oracle_solve_batch(const mcpx_desc* d, const double* theta, const double* x0,
+                       const double* y0, const double* s0, const mcpx_params* p,
+                       mcpx_out* o, int nthreads) {
+  if (!d || !theta || !p || !outputs_ok(o)) return MCPX_EINVAL;
+  const int64_t pd = oracle_theta_dim(d->family, d->n, d->m);
+  if (pd < 0 || d->n + d->m < 1 || d->batch < 0 || d->theta_ld < pd) return MCPX_EINVAL;
+  if (p->linear_solver == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP) return MCPX_EINVAL;
+  return run_batch(d, theta, x0, y0, s0, p, o, nthreads, NULL);
+}
+
+/* MCPX_FAMILY_NONLINEAR: the same with the problem's generated evaluation code. */
+int oracle_solve_batch_nl(const mcpx_desc* d, const double* theta, const double* x0,
+                          const double* y0, const double* s0, const mcpx_params* p,
+                          mcpx_out* o, int nthreads, const oracle_nl* nl) {
+  if (!d || !theta || !p || !outputs_ok(o) || !nl || !nl->init || !nl->eval) return MCPX_EINVAL;
+  if (d->family != MCPX_FAMILY_NONLINEAR || d->n + d->m < 1 || d->batch < 0 || d->theta_ld < nl->p)
+    return MCPX_EINVAL;
+  if (p->linear_solver == MCPX_LINSOLVE_SCHUR && nl->has_s) return MCPX_EINVAL;
+  return run_batch(d, theta, x0, y0, s0, p, o, nthreads, nl);
 }
 
 /* ======================================================================

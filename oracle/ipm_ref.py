@@ -96,10 +96,46 @@ class Solution:
     alpha_trace: list
 
 
-def solve(family, theta, n, m, *, x0=None, y0=None, s0=None, tol=1e-4, max_inner_iters=20,
-          max_outer_iters=50, tightening_rate=0.1, loosening_rate=0.5, min_stepsize=1e-4):
-    """src/solver.jl:35-122 for one instance."""
+def solve(family, theta, n, m, **kw):
+    """src/solver.jl:35-122 for one instance of the QP / affine family."""
     blocks = unpack(family, theta, n, m)
+    return solve_fj(lambda x, y, s, eps: F_and_jacobian(blocks, x, y, s, eps), n, m, **kw)
+
+
+def nl_callbacks(G, H, xs, ys, ts):
+    """Independent evaluation of a nonlinear MCP — sympy.lambdify of G, H and their
+    Jacobian, sharing nothing with the generated C of mcp_amd/codegen.py: returns
+    θ ↦ FJ(x, y, s, ϵ) = (F, ∇F_z) for solve_fj (src/mcp.jl:72-120)."""
+    import sympy as sp
+
+    n, m = len(xs), len(ys)
+    zs = list(xs) + list(ys)
+    args = zs + list(ts)
+    GH = list(G) + list(H)
+    f = sp.lambdify(args, GH, "numpy")
+    jac = sp.lambdify(args, sp.Matrix(GH).jacobian(zs), "numpy")
+
+    def bind(theta):
+        th = [float(t) for t in np.asarray(theta, dtype=np.float64)]
+
+        def FJ(x, y, s, eps):
+            a = [float(v) for v in x] + [float(v) for v in y] + th
+            gh = np.array(f(*a), dtype=np.float64).reshape(n + m)
+            J = np.zeros((n + 2 * m, n + 2 * m))
+            J[:n + m, :n + m] = np.array(jac(*a), dtype=np.float64).reshape(n + m, n + m)
+            J[n:n + m, n + m:] = -np.eye(m)
+            J[n + m:, n:n + m] = np.diag(s)
+            J[n + m:, n + m:] = np.diag(y)
+            return np.concatenate([gh[:n], gh[n:] - s, s * y - eps]), J
+
+        return FJ
+
+    return bind
+
+
+def solve_fj(FJ, n, m, *, x0=None, y0=None, s0=None, tol=1e-4, max_inner_iters=20, max_outer_iters=50,
+             tightening_rate=0.1, loosening_rate=0.5, min_stepsize=1e-4):
+    """The loop of src/solver.jl:35-122 on a callback FJ(x, y, s, ϵ) → (F, ∇F_z)."""
     N = n + 2 * m
     x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64)
     y = np.ones(m) if y0 is None else np.array(y0, dtype=np.float64)
@@ -114,7 +150,7 @@ def solve(family, theta, n, m, *, x0=None, y0=None, s0=None, tol=1e-4, max_inner
         inner_iters = 1
         status = "solved"
         while kkt_error > eps and inner_iters < max_inner_iters:
-            F, J = F_and_jacobian(blocks, x, y, s, eps)
+            F, J = FJ(x, y, s, eps)
             A = J + tol * np.eye(N)
             try:
                 with np.errstate(all="ignore"):

@@ -121,10 +121,13 @@ def test_symbolic_constructors():
     np.testing.assert_array_equal(mcp2.theta_map(θ)[0], readme_qp_theta(θ))
 
 
-def test_non_affine_needs_general_codegen():
-    with pytest.raises(NotAffineError):
-        PrimalDualMCP(lambda x, y, θ: x ** 3 - θ, lambda x, y, θ: x - y, unconstrained_dimension=1,
-                      constrained_dimension=1, parameter_dimension=1)
+def test_non_affine_goes_to_the_nonlinear_family():
+    """G/H that are not affine become generated device code (MCPX_FAMILY_NONLINEAR)."""
+    mcp = PrimalDualMCP(lambda x, y, θ: x ** 3 - θ, lambda x, y, θ: x - y, unconstrained_dimension=1,
+                        constrained_dimension=1, parameter_dimension=1)
+    assert mcp.family == _abi.FAMILY_NONLINEAR and mcp.nl.has_s  # H = x − y depends on y
+    assert mcp.nl.default_solver() == "reduced"
+    assert issubclass(NotAffineError, NotImplementedError)
 
 
 def test_bounds_assertion():

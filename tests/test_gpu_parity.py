@@ -59,7 +59,7 @@ def _params_from(d):
 LS = ["reduced", "dense", "schur"]
 
 
-@pytest.mark.parametrize("path", sorted(p for p in glob.glob(os.path.join(HERE, "golden", "*.npz")) if not os.path.basename(p).startswith("sens_")),
+@pytest.mark.parametrize("path", sorted(p for p in glob.glob(os.path.join(HERE, "golden", "*.npz")) if not os.path.basename(p).startswith(("sens_", "nl_"))),
                          ids=lambda p: os.path.basename(p)[:-4])
 @pytest.mark.parametrize("variant", ["specialized", "generic"])  # MCPX_GENERIC_KERNELS A/B
 def test_golden(gpu, path, variant, monkeypatch):

@@ -14,7 +14,7 @@ from mcp_amd.qp_benchmark import generate_random_parameter
 from oracle import ipm_ref
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-GOLDEN = sorted(p for p in glob.glob(os.path.join(HERE, "golden", "*.npz")) if not os.path.basename(p).startswith("sens_"))
+GOLDEN = sorted(p for p in glob.glob(os.path.join(HERE, "golden", "*.npz")) if not os.path.basename(p).startswith(("sens_", "nl_")))
 FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters", "active_mask")
 
 
