@@ -43,7 +43,7 @@ def pmc_traffic(n: int, m: int, B: int, ls: str):
         return None, None
     want = {"schur": 2, "reduced": 0, "dense": 1}[ls]
     k = d.get("kernel", "")
-    if int(d.get("Grid_Size", 0)) != 64 * B or f", 0, {n}, {m}, {want}>" not in k:
+    if int(d.get("Grid_Size", 0)) != 64 * B or f", 0, {n}, {m}, {want}" not in k:
         return None, None
     return (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0, os.path.relpath(PMC_SUMMARY, ROOT)
 
@@ -87,7 +87,111 @@ def parse():
                          "f = Σx² + Σy² (src/AutoDiff.jl:42-82, test/runtests.jl:72-75)")
     ap.add_argument("--gather", action="store_true",
                     help="run the RCCL result collection even at world size 1 (rehearsal under torchrun)")
+    ap.add_argument("--lane-change", type=int, default=0, metavar="T",
+                    help="BASELINE C4: each step solves --batch lane-change games of horizon T (generated "
+                         "nonlinear module; examples/lane_change.jl, benchmark/trajectory_game_benchmark.jl)")
     return ap.parse_args()
+
+
+def main_lane_change(a):
+    """BASELINE C4: B lane-change trajectory games (θ from the sampler of
+    benchmark/trajectory_game_benchmark.jl:62-87) solved per step by the generated
+    nonlinear module, x₀ = y₀ = s₀ defaults and tol as benchmark/path.jl:8,67-84.
+    Instances shard over ranks (weak scaling); no collective on the data path."""
+    import torch
+    import torch.distributed as dist
+
+    from mcp_amd import _abi
+    from mcp_amd.batch import alloc_device_outputs, solve_batch_device
+    from mcp_amd.lane_change import LaneChangeGame
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("NCCL_DEBUG", "WARN")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    game = LaneChangeGame(a.lane_change)
+    mcp = game.mcp
+    n, m, B = mcp.unconstrained_dimension, mcp.constrained_dimension, a.batch
+    N = n + 2 * m
+    module = mcp.module()
+    rng = np.random.default_rng(np.random.SeedSequence(a.seed, spawn_key=(rank,)))
+    theta_host = np.ascontiguousarray(mcp.theta_map(game.generate_random_parameter(rng, B)))
+    theta = torch.from_numpy(theta_host).to(dev)
+    out = alloc_device_outputs(B, n, m, dev)
+    stream = torch.cuda.current_stream(dev)
+    ls = mcp.nl.default_solver()
+
+    def step():
+        solve_batch_device(_abi.FAMILY_NONLINEAR, n, m, theta, out, tol=a.tol, linear_solver=ls, stream=stream,
+                           module=module)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    newton = out["newton_iters"].to(torch.float64).sum().item()
+    solved = (out["status"] == 0).to(torch.float64).mean().item()
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms, newton, solved], dtype=torch.float64, device=dev)
+        t2 = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t2, op=dist.ReduceOp.SUM)
+        elapsed, kern_ms, newton, solved = float(t[0]), float(t[1]), float(t2[2]), float(t2[3]) / world
+    if rank == 0:
+        flops_launch = newton / world * lu_flops(N)
+        achieved = flops_launch / (kern_ms * 1e-3) / 1e12
+        res = {
+            "metric": "MCP solves/sec (lane-change trajectory game, generated nonlinear module)",
+            "value": a.steps * B * world / elapsed, "unit": "solves/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic θ (benchmark/trajectory_game_benchmark.jl:62-87 sampler, numpy PCG64 "
+                    f"SeedSequence({a.seed}, spawn_key=(rank,))), uploaded to HBM before timing",
+            "config": {"workload": f"BASELINE C4: 2-player lane-change game T={a.lane_change} "
+                                   f"(n={n}, m={m}, KKT dim {N}), fp64, {B} games per GPU, tol={a.tol:g}",
+                       "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "batch_per_gpu": B,
+                       "global_batch": B * world, "parallelism": f"dp{world} (instance shards)"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": "mcpx_nl_solve_" + ls,
+                         "kernel_ms": kern_ms, "flops_per_launch": flops_launch,
+                         "note": f"SURVEY.md §8(d) algorithmic FLOPs: dense LU of the N={N} KKT system per "
+                                 "Newton step x the run's own Newton counts / HIP-event kernel time"},
+            "newton_iters_mean": newton / (B * world), "success_rate": solved,
+        }
+        if world == 1 and a.cpu_sample > 0:
+            from oracle import coracle
+
+            coracle.build()
+            th = int(a.cpu_threads) or min(16, os.cpu_count() or 1)
+            S = min(a.cpu_sample, B)
+            t1 = time.perf_counter()
+            r = coracle.solve_batch_nl(mcp.nl, theta_host[:S], tol=a.tol, linear_solver=ls, nthreads=th)
+            dt = time.perf_counter() - t1
+            res["cpu_baseline"] = dict(value=S / dt, unit="solves/s", cores=th, kind="port",
+                                       sample=f"first {S} games of rank 0, C oracle with the generated host "
+                                              f"G/H code, {th} threads, {dt:.2f} s wall",
+                                       status_match=bool(np.array_equal(r["status"],
+                                                                        out["status"][:S].cpu().numpy())))
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def cpu_baseline(theta_host: np.ndarray, n: int, m: int, tol: float, threads: int, ls: str) -> dict:
@@ -115,6 +219,8 @@ def cpu_baseline(theta_host: np.ndarray, n: int, m: int, tol: float, threads: in
 
 def main():
     a = parse()
+    if a.lane_change:
+        return main_lane_change(a)
     import torch
     import torch.distributed as dist
 
