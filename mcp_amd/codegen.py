@@ -56,7 +56,7 @@ GEN_DIR = os.environ.get("MCPX_GEN_DIR") or os.path.join(HERE, "_gen")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
-GEN_VERSION = 1
+GEN_VERSION = 2
 LDS_LIMIT = 160 * 1024 - 2048  # bytes of static LDS one workgroup may declare on gfx950 (minus headroom)
 
 _FUNCS = {  # sympy function → C name (both libm and HIP device math)
