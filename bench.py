@@ -157,6 +157,15 @@ def main_lane_change(a):
     if rank == 0:
         flops_launch = newton / world * lu_flops(N)
         achieved = flops_launch / (kern_ms * 1e-3) / 1e12
+        traffic, traffic_src = None, None
+        pmc_path = os.path.join(ROOT, "profiles", "r01", "pmc_c4_lane.json")
+        try:  # tools/gpu_c4_pmc.sh on this exact configuration: (FETCH_SIZE + WRITE_SIZE) KB per launch
+            d = json.load(open(pmc_path))
+            if d.get("kernel") == "mcpx_nl_solve_" + ls and int(d.get("Grid_Size", 0)) == 64 * B \
+                    and a.lane_change == 2:
+                traffic, traffic_src = (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0, os.path.relpath(pmc_path, ROOT)
+        except (OSError, ValueError, KeyError):
+            pass
         res = {
             "metric": "MCP solves/sec (lane-change trajectory game, generated nonlinear module)",
             "value": a.steps * B * world / elapsed, "unit": "solves/s", "n_gpus": world, "steps": a.steps,
@@ -169,7 +178,8 @@ def main_lane_change(a):
                        "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "batch_per_gpu": B,
                        "global_batch": B * world, "parallelism": f"dp{world} (instance shards)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": "mcpx_nl_solve_" + ls,
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "mcpx_nl_solve_" + ls,
                          "kernel_ms": kern_ms, "flops_per_launch": flops_launch,
                          "note": f"SURVEY.md §8(d) algorithmic FLOPs: dense LU of the N={N} KKT system per "
                                  "Newton step x the run's own Newton counts / HIP-event kernel time"},
