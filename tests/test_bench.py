@@ -53,3 +53,15 @@ def test_cli_has_every_baseline_mode():
                          text=True, check=True).stdout
     for flag in ("--gpus", "--steps", "--warmup", "--sens", "--lane-change", "--gather", "--cpu-sample"):
         assert flag in out
+
+
+@pytest.mark.gpu
+def test_gpu_bench_lane_change_line():
+    """The C4 bench line on a small batch: one JSON line, statuses equal to the C oracle's."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--lane-change", "2", "--batch", "64",
+                        "--steps", "1", "--warmup", "1", "--cpu-sample", "64"], capture_output=True, text=True,
+                       timeout=110, check=True)
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["config"]["kkt_dim"] == 140 and d["n_gpus"] == 1
+    assert d["value"] > 0 and 0 < d["roofline"]["frac"] < 1
+    assert d["cpu_baseline"]["status_match"] is True
