@@ -1,17 +1,28 @@
 """Benchmark: batched interior-point MCP solves on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--n 32 --m 16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch G | --batch B] ...
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
 A "step" is one full batched solve (src/solver.jl:35-122 for every instance:
-ϵ-continuation, Newton steps, LU, line search) of B random dense QP-KKT
-instances per GPU (benchmark/quadratic_program_benchmark.jl family, fp64,
-tol = 1e-6 as benchmark/path.jl:8), θ generated on the host (numpy PCG64,
-documented seed) and uploaded before the timed region, so it is
-resident in HBM when timing starts; with N > 1
-ranks each rank solves its own shard (weak scaling: B instances per GPU) and
-the packed per-instance results are all-gathered over RCCL (north_star:
-collective only for solution collection).  Rank 0 prints one JSON line.
+ϵ-continuation, Newton steps, linear solve, line search) of random dense QP-KKT
+instances (benchmark/quadratic_program_benchmark.jl family, fp64, tol = 1e-6 as
+benchmark/path.jl:8).  θ is generated on the host (numpy PCG64 in chunks of
+4096 instances, chunk c seeded SeedSequence(seed, spawn_key=(c,)), so instance i
+is the same at every GPU count) and uploaded before the timed region, so it is
+resident in HBM when timing starts.
+
+Workload (BASELINE.json configs):
+  default         C3: global batch 65,536 (n=32, m=16, KKT dim 64), sharded over
+                  the N GPUs (strong scaling: 65,536 at N=1, 8,192 per GPU at N=8);
+  --batch B       B instances per GPU instead (weak scaling);
+  --sens          C5: solve + rrule pullback (VJP kernel), global batch 4,096;
+  --lane-change T C4: the lane-change trajectory game, global batch 1,024.
+With N > 1 ranks the packed per-instance results are all-gathered over RCCL
+inside the timed step (north_star: collective only for solution collection).
+
+`--gpus N` without torchrun's RANK in the environment starts N ranks itself
+(torch.distributed.run as a child process, before this process touches the
+GPU) and fails if fewer than N GPUs are visible.  Rank 0 prints one JSON line.
 """
 
 from __future__ import annotations
@@ -19,6 +30,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,24 +41,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "MCP solves/sec (batched QP-KKT, n=64) at 1/2/4/8 GPUs; % LU roofline"
-FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (AMD datasheet)
-# rocprofv3 PMC pass of this same bench command (tools/gpu_profile.sh), per kernel dispatch
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_c3_schur.json")
-
-
-def pmc_traffic(n: int, m: int, B: int, ls: str):
-    """HBM-side bytes per launch from the committed PMC summary when it was taken on
-    this exact configuration: (FETCH_SIZE + WRITE_SIZE) KB × 1024.  FETCH_SIZE counts
-    L2 misses served by the Infinity Cache too (MI355X_MICROARCH.md, HBM section)."""
-    try:
-        d = json.load(open(PMC_SUMMARY))
-    except (OSError, ValueError):
-        return None, None
-    want = {"schur": 2, "reduced": 0, "dense": 1}[ls]
-    k = d.get("kernel", "")
-    if int(d.get("Grid_Size", 0)) != 64 * B or f", 0, {n}, {m}, {want}" not in k:
-        return None, None
-    return (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0, os.path.relpath(PMC_SUMMARY, ROOT)
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+# rocprofv3 evidence of this round's kernels (tools/gpu_profile.sh + tools/prof_summary.py)
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+DEFAULT_GLOBAL = {"c3": 65536, "c5": 4096, "c4": 1024}
 
 
 def lu_flops(N: int) -> float:
@@ -63,205 +63,342 @@ def solve_dim(n: int, m: int, linear_solver: str) -> int:
 
 def executed_flops(n: int, m: int, linear_solver: str) -> float:
     """FLOPs the kernel actually spends on the Newton linear solve per step: the LU of
-    the factored system, plus the Schur-complement GEMM (2n²m, fp64 MFMA) for schur."""
+    the factored system, plus the Schur-complement GEMM (2n²m) for schur."""
     f = lu_flops(solve_dim(n, m, linear_solver))
     return f + (2.0 * n * n * m if linear_solver == "schur" else 0.0)
 
 
-def parse():
+def roofline_bound(linear_solver: str) -> str:
+    """What limits the solve kernels (PMC evidence): the register LU /
+    Gauss-Jordan is FP64-VALU-issue-bound; θ traffic is ≤ 1/5 of HBM peak."""
+    return "valu"
+
+
+def host_cpus() -> dict:
+    """CPUs this process can actually use: its affinity set, capped by the cgroup CPU
+    quota (a GPU box grants 16 of the machine's 256 hardware threads; GNU `nproc`
+    prints 16 there too, via OMP_NUM_THREADS), plus the machine total and model."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    info = {"affinity_cpus": affinity, "machine_cpus": os.cpu_count()}
+    usable = affinity
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q and q[0] != "max":
+            info["cgroup_cpus"] = float(q[0]) / float(q[1])
+            usable = max(1, min(usable, int(info["cgroup_cpus"] + 0.999)))
+    except (OSError, ValueError, IndexError):
+        pass
+    info["nproc"] = usable
+    try:
+        info["model"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return info
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="instances over all GPUs, sharded (strong scaling); 0 = the BASELINE config's")
+    ap.add_argument("--batch", type=int, default=0, help="instances per GPU (weak scaling) instead")
     ap.add_argument("--n", type=int, default=32)
     ap.add_argument("--m", type=int, default=16)
     ap.add_argument("--tol", type=float, default=1e-6)
     ap.add_argument("--sparsity", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--linear-solver", default="schur", choices=["reduced", "dense", "schur"])
-    ap.add_argument("--cpu-sample", type=int, default=32768, help="instances in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="instances in the CPU-baseline sample (-1 = 2048 per thread, 0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use (nproc)")
+    ap.add_argument("--host-runs", type=int, default=5, help="timed runs of the host-buffer API (median)")
     ap.add_argument("--sens", action="store_true",
                     help="BASELINE C5: each step is the batched solve + the rrule pullback (VJP kernel) of "
                          "f = Σx² + Σy² (src/AutoDiff.jl:42-82, test/runtests.jl:72-75)")
     ap.add_argument("--gather", action="store_true",
                     help="run the RCCL result collection even at world size 1 (rehearsal under torchrun)")
     ap.add_argument("--lane-change", type=int, default=0, metavar="T",
-                    help="BASELINE C4: each step solves --batch lane-change games of horizon T (generated "
+                    help="BASELINE C4: each step solves lane-change games of horizon T (generated "
                          "nonlinear module; examples/lane_change.jl, benchmark/trajectory_game_benchmark.jl)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main_lane_change(a):
-    """BASELINE C4: B lane-change trajectory games (θ from the sampler of
+def mode_of(a) -> str:
+    return "c4" if a.lane_change else ("c5" if a.sens else "c3")
+
+
+def plan(a, world: int, rank: int) -> dict:
+    """This rank's instances: a contiguous shard of the global batch (strong scaling,
+    the BASELINE configs) or `--batch` per GPU (weak scaling)."""
+    from mcp_amd.distributed import shard_capacity, shard_range
+
+    if a.batch > 0:
+        return dict(start=rank * a.batch, count=a.batch, cap=a.batch, global_batch=a.batch * world,
+                    scaling="weak")
+    G = a.global_batch or DEFAULT_GLOBAL[mode_of(a)]
+    start, count = shard_range(G, world, rank)
+    return dict(start=start, count=count, cap=shard_capacity(G, world), global_batch=G, scaling="strong")
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(nranks: int, script: str, argv, have_devices: int | None = None) -> int:
+    """`--gpus N` outside torchrun: N ranks of `script`, one per GPU, through
+    torch.distributed.run started as a child process; this process only counts the
+    devices (torch.cuda.device_count does not initialise the GPU) and fails if fewer
+    than N are visible.  Returns the child's exit code."""
+    if have_devices is None:
+        import torch
+
+        have_devices = torch.cuda.device_count()
+    if have_devices < nranks:
+        print(f"bench.py: --gpus {nranks} but only {have_devices} GPU(s) are visible", file=sys.stderr)
+        return 2
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), script, *argv]
+    return subprocess.call(cmd, env=env)
+
+
+def evidence(name: str, cfg: dict) -> dict:
+    """The committed rocprofv3 summaries of this configuration (profiles/r02/
+    trace_<name>.json, pmc_<name>.json; tools/prof_summary.py), if they were taken on
+    exactly this configuration and this build of libmcpx.so; else {}."""
+    from mcp_amd.build import built_hash
+
+    out = {}
+    for kind in ("trace", "pmc"):
+        path = os.path.join(PROFILE_DIR, f"{kind}_{name}.json")
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") != cfg or d.get("lib_hash") != built_hash():
+            continue
+        d["_source"] = os.path.relpath(path, ROOT)
+        out[kind] = d
+    return out
+
+
+def evidence_id(key: str, cfg: dict) -> dict:
+    """What tools/prof_summary.py stamps on the profile summaries of this run."""
+    from mcp_amd.build import built_hash
+
+    return {"key": key, "config": cfg, "lib_hash": built_hash()}
+
+
+def pmc_traffic(ev: dict):
+    """HBM-side bytes per launch of the dominant kernel from the PMC summary:
+    (FETCH_SIZE + WRITE_SIZE) KB × 1024 (MI355X_MICROARCH.md: FETCH_SIZE also counts
+    reads served by the Infinity Cache)."""
+    p = ev.get("pmc")
+    if not p or "FETCH_SIZE" not in p or "WRITE_SIZE" not in p:
+        return None, None
+    return (p["FETCH_SIZE"] + p["WRITE_SIZE"]) * 1024.0, p["_source"]
+
+
+def summary_statistics(step_s, count: int, success_rate: float) -> dict:
+    """benchmark/path.jl:101-126 (summary_statistics / runtime_stats / fraction_solved)
+    for a batched solver: the reference times each solve alone; a batched step solves
+    `count` instances at once, so μ and σ are the per-step device times (HIP events)
+    ÷ count (seconds per solve, amortised over the batch) over the timed steps."""
+    per = np.asarray(step_s, dtype=np.float64) / max(count, 1)
+    return {"ip": {"success_rate": success_rate, "μ": float(per.mean()),
+                   "σ": float(per.std(ddof=1)) if len(per) > 1 else 0.0,
+                   "unit": "s per solve (step time / instances per GPU)", "steps": len(per)}}
+
+
+def cpu_baseline(solve, count_avail: int, a, threads_all: int, label: str) -> dict:
+    """Times the C oracle (the same algorithm as the kernel, oracle/ipm_oracle.c) on
+    every CPU this process may use, on a bounded sample of the workload, plus one
+    core alone.  `solve(k, threads)` solves the first k instances."""
+    solve(min(64, count_avail), threads_all)  # warm: library load, generated code compiled
+    S = min(count_avail, a.cpu_sample if a.cpu_sample > 0 else 2048 * threads_all)
+    t0 = time.perf_counter()
+    r = solve(S, threads_all)
+    dt = time.perf_counter() - t0
+    S1 = min(count_avail, max(64, S // max(threads_all, 1)))
+    t1 = time.perf_counter()
+    solve(S1, 1)
+    dt1 = time.perf_counter() - t1
+    info = host_cpus()
+    return dict(value=S / dt, unit="solves/s", cores=threads_all, kind="port",
+                single_core_value=S1 / dt1, nproc=info["nproc"], machine_cpus=info["machine_cpus"],
+                affinity_cpus=info["affinity_cpus"], host_cpu=info.get("model", ""),
+                cgroup_cpus=info.get("cgroup_cpus"),
+                sample=f"{S} instances of the same workload (the first {S} of rank 0), {label}, "
+                       f"{threads_all} threads = usable CPUs (cgroup quota / affinity), {dt:.2f} s wall; single core: {S1} instances in {dt1:.2f} s",
+                _result=r)
+
+
+def timed_steps(step, a, stream, world, dist, dev, sub_events: int = 1):
+    """W untimed warm-up steps, then exactly K steps between barrier + synchronize;
+    HIP events around each launch, recorded on the kernels' own stream.  Returns
+    (elapsed wall time of the K steps, per-launch ms lists, one per event pair)."""
+    import torch
+
+    for _ in range(a.warmup):
+        step(None)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+          for _ in range(sub_events)]
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step([e[i] for e in ev])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    return elapsed, [[s.elapsed_time(e) for s, e in evs] for evs in ev]
+
+
+def reduce_max_sum(dist, dev, world, maxes, sums):
+    import torch
+
+    if world == 1:
+        return list(maxes), list(sums)
+    t = torch.tensor(list(maxes), dtype=torch.float64, device=dev)
+    s = torch.tensor(list(sums), dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    return t.tolist(), s.tolist()
+
+
+def roofline(kern_ms: float, flops_launch: float, exec_flops_launch: float, alg_bytes: float, ev: dict,
+             kernel: str, bound: str, note: str) -> dict:
+    achieved = flops_launch / (kern_ms * 1e-3) / 1e12
+    executed = exec_flops_launch / (kern_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(ev)
+    r = {"bound": bound, "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+         "executed_tflops": executed, "executed_frac": executed / FP64_PEAK_TFLOPS,
+         "algorithmic_bytes": alg_bytes, "hbm_gbs_algorithmic": alg_bytes / (kern_ms * 1e-3) / 1e9,
+         "kernel": kernel, "kernel_ms": kern_ms, "flops_per_launch": flops_launch,
+         "executed_flops_per_launch": exec_flops_launch, "note": note}
+    tr = ev.get("trace")
+    if tr:
+        t_ms = float(tr.get("launch_avg_ms_all_passes", tr["avg_ms"]))
+        r.update(trace_kernel_ms=t_ms, frac_trace=flops_launch / (t_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                 executed_frac_trace=exec_flops_launch / (t_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                 trace_source=tr["_source"])
+    if traffic:
+        r["traffic_over_algorithmic"] = traffic / alg_bytes
+    return r
+
+
+def main_lane_change(a, world, rank, local, dist, pl):
+    """BASELINE C4: lane-change trajectory games (θ from the sampler of
     benchmark/trajectory_game_benchmark.jl:62-87) solved per step by the generated
     nonlinear module, x₀ = y₀ = s₀ defaults and tol as benchmark/path.jl:8,67-84.
-    Instances shard over ranks (weak scaling); no collective on the data path."""
+    Instances shard over ranks; no collective on the data path."""
     import torch
-    import torch.distributed as dist
 
     from mcp_amd import _abi
     from mcp_amd.batch import alloc_device_outputs, solve_batch_device
     from mcp_amd.lane_change import LaneChangeGame
+    from mcp_amd.qp_benchmark import chunked_slice
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("NCCL_DEBUG", "WARN")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     game = LaneChangeGame(a.lane_change)
     mcp = game.mcp
-    n, m, B = mcp.unconstrained_dimension, mcp.constrained_dimension, a.batch
+    n, m, B = mcp.unconstrained_dimension, mcp.constrained_dimension, pl["count"]
     N = n + 2 * m
     module = mcp.module()
-    rng = np.random.default_rng(np.random.SeedSequence(a.seed, spawn_key=(rank,)))
-    theta_host = np.ascontiguousarray(mcp.theta_map(game.generate_random_parameter(rng, B)))
+    theta_host = np.ascontiguousarray(mcp.theta_map(
+        chunked_slice(lambda rng, k: game.generate_random_parameter(rng, k), a.seed, pl["start"], B)))
     theta = torch.from_numpy(theta_host).to(dev)
     out = alloc_device_outputs(B, n, m, dev)
     stream = torch.cuda.current_stream(dev)
     ls = mcp.nl.default_solver()
 
-    def step():
+    def step(evs):
+        if evs:
+            evs[0][0].record(stream)
         solve_batch_device(_abi.FAMILY_NONLINEAR, n, m, theta, out, tol=a.tol, linear_solver=ls, stream=stream,
                            module=module)
+        if evs:
+            evs[0][1].record(stream)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    elapsed, ms = timed_steps(step, a, stream, world, dist, dev)
+    kern_ms = float(np.mean(ms[0]))
+    step_s = [t * 1e-3 for t in ms[0]]
     newton = out["newton_iters"].to(torch.float64).sum().item()
-    solved = (out["status"] == 0).to(torch.float64).mean().item()
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms, newton, solved], dtype=torch.float64, device=dev)
-        t2 = t.clone()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t2, op=dist.ReduceOp.SUM)
-        elapsed, kern_ms, newton, solved = float(t[0]), float(t[1]), float(t2[2]), float(t2[3]) / world
-    if rank == 0:
-        flops_launch = newton / world * lu_flops(N)
-        achieved = flops_launch / (kern_ms * 1e-3) / 1e12
-        traffic, traffic_src = None, None
-        pmc_path = os.path.join(ROOT, "profiles", "r01", "pmc_c4_lane.json")
-        try:  # tools/gpu_c4_pmc.sh on this exact configuration: (FETCH_SIZE + WRITE_SIZE) KB per launch
-            d = json.load(open(pmc_path))
-            if d.get("kernel") == "mcpx_nl_solve_" + ls and int(d.get("Grid_Size", 0)) == 64 * B \
-                    and a.lane_change == 2:
-                traffic, traffic_src = (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0, os.path.relpath(pmc_path, ROOT)
-        except (OSError, ValueError, KeyError):
-            pass
-        res = {
-            "metric": "MCP solves/sec (lane-change trajectory game, generated nonlinear module)",
-            "value": a.steps * B * world / elapsed, "unit": "solves/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic θ (benchmark/trajectory_game_benchmark.jl:62-87 sampler, numpy PCG64 "
-                    f"SeedSequence({a.seed}, spawn_key=(rank,))), uploaded to HBM before timing",
-            "config": {"workload": f"BASELINE C4: 2-player lane-change game T={a.lane_change} "
-                                   f"(n={n}, m={m}, KKT dim {N}), fp64, {B} games per GPU, tol={a.tol:g}",
-                       "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "batch_per_gpu": B,
-                       "global_batch": B * world, "parallelism": f"dp{world} (instance shards)"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "mcpx_nl_solve_" + ls,
-                         "kernel_ms": kern_ms, "flops_per_launch": flops_launch,
-                         "note": f"SURVEY.md §8(d) algorithmic FLOPs: dense LU of the N={N} KKT system per "
-                                 "Newton step x the run's own Newton counts / HIP-event kernel time"},
-            "newton_iters_mean": newton / (B * world), "success_rate": solved,
-        }
-        if world == 1 and a.cpu_sample > 0:
-            from oracle import coracle
+    solved = (out["status"] == 0).to(torch.float64).sum().item()
+    (elapsed, kern_ms), (newton_all, solved_all) = reduce_max_sum(dist, dev, world, [elapsed, kern_ms],
+                                                                  [newton, solved])
+    if rank != 0:
+        return
+    cfg = {"mode": "c4", "horizon": a.lane_change, "batch_per_gpu": B, "linear_solver": ls}
+    key = f"c4_lane_t{a.lane_change}_b{B}"
+    ev = evidence(key, cfg)
+    kernel = "mcpx_nl_solve_" + ls
+    rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
+                  B * 8.0 * (mcp.nl.p + n + 2 * m + 2) + 12.0 * B, ev, kernel, "latency",
+                  f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system per Newton step) "
+                  f"x rank 0's own Newton counts / HIP-event kernel time; executed = what the kernel performs "
+                  f"({ls}: LU of dim {solve_dim(n, m, ls)}" + (" + 2n^2m Schur formation" if ls == "schur" else "")
+                  + "); bound: per-wave latency (PMC: waves stall on LDS/VALU dependencies, DESIGN.md §4)")
+    res = {
+        "metric": "MCP solves/sec (lane-change trajectory game, generated nonlinear module)",
+        "value": a.steps * pl["global_batch"] / elapsed, "unit": "solves/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
+        "scaling": pl["scaling"], "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic θ (benchmark/trajectory_game_benchmark.jl:62-87 sampler, numpy PCG64 in chunks of 4096 "
+                f"seeded SeedSequence({a.seed}, spawn_key=(chunk,))), uploaded to HBM before timing",
+        "config": {"workload": f"BASELINE C4: 2-player lane-change game T={a.lane_change} "
+                               f"(n={n}, m={m}, KKT dim {N}), fp64, global batch {pl['global_batch']}, tol={a.tol:g}",
+                   "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "batch_per_gpu": B,
+                   "global_batch": pl["global_batch"], "parallelism": f"dp{world} (instance shards)"},
+        "roofline": rl,
+        "newton_iters_mean": newton_all / pl["global_batch"], "success_rate": solved_all / pl["global_batch"],
+        "summary_statistics": summary_statistics(step_s, B, solved_all / pl["global_batch"]),
+        "evidence": evidence_id(key, cfg),
+    }
+    if world == 1 and a.cpu_sample != 0:
+        from oracle import coracle
 
-            coracle.build()
-            th = int(a.cpu_threads) or min(16, os.cpu_count() or 1)
-            S = min(a.cpu_sample, B)
-            t1 = time.perf_counter()
-            r = coracle.solve_batch_nl(mcp.nl, theta_host[:S], tol=a.tol, linear_solver=ls, nthreads=th)
-            dt = time.perf_counter() - t1
-            res["cpu_baseline"] = dict(value=S / dt, unit="solves/s", cores=th, kind="port",
-                                       sample=f"first {S} games of rank 0, C oracle with the generated host "
-                                              f"G/H code, {th} threads, {dt:.2f} s wall",
-                                       status_match=bool(np.array_equal(r["status"],
-                                                                        out["status"][:S].cpu().numpy())))
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        coracle.build()
+        th = a.cpu_threads or host_cpus()["nproc"]
+        cb = cpu_baseline(lambda k, t: coracle.solve_batch_nl(mcp.nl, theta_host[:k], tol=a.tol, linear_solver=ls,
+                                                              nthreads=t),
+                          B, a, th, "C oracle with the generated host G/H code (same algorithm and linear solver)")
+        r = cb.pop("_result")
+        cb["status_match"] = bool(np.array_equal(r["status"], out["status"][:len(r["status"])].cpu().numpy()))
+        res["cpu_baseline"] = cb
+    print(json.dumps(res), flush=True)
 
 
-def cpu_baseline(theta_host: np.ndarray, n: int, m: int, tol: float, threads: int, ls: str) -> dict:
-    """Times the C oracle (oracle/ipm_oracle.c, same algorithm) on host cores."""
-    from oracle import coracle
-
-    coracle.build()
-    coracle.solve_batch(0, n, m, theta_host[: min(64, len(theta_host))], tol=tol, nthreads=threads,
-                        linear_solver=ls)  # warm
-    t0 = time.perf_counter()
-    r = coracle.solve_batch(0, n, m, theta_host, tol=tol, nthreads=threads, linear_solver=ls)
-    dt = time.perf_counter() - t0
-    model = ""
-    try:
-        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
-    return dict(value=len(theta_host) / dt, unit="solves/s", cores=threads, kind="port",
-                host_cpu=model, host_nproc=os.cpu_count(),
-                sample=f"{len(theta_host)} instances of the same workload (first {len(theta_host)} θ of rank 0), "
-                       f"C oracle (oracle/ipm_oracle.c, same algorithm and linear solver) on {threads} host threads, "
-                       f"{dt:.2f} s wall = {dt * threads:.1f} thread-s",
-                newton_mean=float(r["newton_iters"].mean()))
-
-
-def main():
-    a = parse()
-    if a.lane_change:
-        return main_lane_change(a)
+def main_qp(a, world, rank, local, dist, pl, distributed):
     import torch
-    import torch.distributed as dist
 
-    from mcp_amd.batch import solve_batch_device
-    from mcp_amd.distributed import Gatherer, alloc_packed
-    from mcp_amd.batch import solve_batch
-    from mcp_amd.qp_benchmark import generate_random_parameter
+    from mcp_amd.batch import solve_batch, solve_batch_device
+    from mcp_amd.distributed import Gatherer, alloc_packed, shard_range
+    from mcp_amd.qp_benchmark import generate_global_slice
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1 or (a.gather and "RANK" in os.environ)
-    if distributed:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("NCCL_DEBUG", "WARN")  # keep RCCL's banner off stdout (one JSON line)
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    n, m, B = a.n, a.m, a.batch
+    n, m, B = a.n, a.m, pl["count"]
     N = n + 2 * m
-
-    # host RNG, one independent stream per rank (SeedSequence(seed, spawn_key=(rank,))), uploaded once
-    rng = np.random.default_rng(np.random.SeedSequence(a.seed, spawn_key=(rank,)))
-    theta_host = generate_random_parameter(rng, n, m, a.sparsity, batch=B)
+    theta_host = generate_global_slice(a.seed, n, m, a.sparsity, pl["start"], B)
     theta = torch.from_numpy(theta_host).to(dev)
     # outputs written straight into one packed fp64 record buffer + one int32 buffer
     # (x | y | s | kkt | ϵ and outer | status | newton), so the collection is 2 all-gathers
-    packed = alloc_packed(B, n, m, dev)
+    packed = alloc_packed(B, n, m, dev, capacity=pl["cap"])
     out = packed.views()
     gather = Gatherer(packed) if distributed else None
-
     stream = torch.cuda.current_stream(dev)
 
     if a.sens:
@@ -281,128 +418,154 @@ def main():
         vjp_batch_device(0, n, m, theta, out["x"], out["y"], out["s"], gx, gy, zeros_m, dtheta, vstat,
                          stream=stream)
 
-    def step():
+    def step(evs):
+        if evs:
+            evs[0][0].record(stream)
         solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
+        if evs:
+            evs[0][1].record(stream)
         if a.sens:
+            if evs:
+                evs[1][0].record(stream)
             pullback()
+            if evs:
+                evs[1][1].record(stream)
         if gather is not None:
             gather()
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if distributed:
-        dist.barrier()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        ev[i][0].record(stream)
-        solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
-        ev[i][1].record(stream)
-        if a.sens:
-            evs[i][0].record(stream)
-            pullback()
-            evs[i][1].record(stream)
-        if gather is not None:
-            gather()
-    torch.cuda.synchronize(dev)
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    vjp_ms = float(np.mean([s.elapsed_time(e) for s, e in evs])) if a.sens else None
+    elapsed, ms = timed_steps(step, a, stream, world, dist, dev, 2 if a.sens else 1)
+    kern_ms = float(np.mean(ms[0]))
+    vjp_ms = float(np.mean(ms[1])) if a.sens else 0.0
+    step_s = [sum(t) * 1e-3 for t in zip(*ms)]  # per-step device time of the solve (+ pullback)
     # PCIe-inclusive rate of the host-buffer API (mcpx_solve_batch: H→D θ, solve, D→H
-    # results) — reported beside `value`, never as it
-    host_rate = None
-    if world == 1:
+    # results), median of --host-runs runs after one warm-up;
+    # reported beside `value`, never as it
+    host = None
+    if world == 1 and a.host_runs > 0 and not a.sens:
         solve_batch(0, n, m, theta_host[:1024], tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
-        t1 = time.perf_counter()
-        solve_batch(0, n, m, theta_host, tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
-        host_rate = B / (time.perf_counter() - t1)
+        runs = []
+        for _ in range(a.host_runs):
+            t1 = time.perf_counter()
+            solve_batch(0, n, m, theta_host, tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
+            runs.append(time.perf_counter() - t1)
+        host = {"median_solves_per_s": B / float(np.median(runs)), "runs_s": runs,
+                "note": "mcpx_solve_batch on host numpy buffers: H->D theta, solve, D->H results"}
     newton = out["newton_iters"].to(torch.float64).sum().item()
-    solved = (out["status"] == 0).to(torch.float64).mean().item()
+    solved = (out["status"] == 0).to(torch.float64).sum().item()
+    (elapsed, kern_ms, vjp_ms), (newton_all, solved_all) = reduce_max_sum(
+        dist, dev, world, [elapsed, kern_ms, vjp_ms], [newton, solved])
     if distributed:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-        s = torch.tensor([newton, solved], dtype=torch.float64, device=dev)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        newton, solved = float(s[0]), float(s[1]) / world
-
-    if rank == 0:
-        NS = solve_dim(n, m, a.linear_solver)
-        # algorithmic FLOPs per Newton step = dense LU of the N = n+2m
-        # KKT system, 2N³/3 + 2N², × the run's own Newton counts, per launch (per GPU)
-        flops_launch = newton / world * lu_flops(N)
-        traffic, traffic_src = pmc_traffic(n, m, B, a.linear_solver)
-        achieved = flops_launch / (kern_ms * 1e-3) / 1e12
-        executed = newton / world * executed_flops(n, m, a.linear_solver) / (kern_ms * 1e-3) / 1e12
-        res = {
-            "metric": METRIC,
-            "value": a.steps * B * world / elapsed,
-            "unit": "solves/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (random dense QPs of benchmark/quadratic_program_benchmark.jl, host numpy PCG64 "
-                    f"SeedSequence({a.seed}, spawn_key=(rank,)), uploaded to HBM before timing)",
-            "config": {"workload": f"BASELINE C3: random dense QP-KKT n={n} m={m} (KKT dim {N}), fp64, "
-                                   f"{B} instances per GPU, tol={a.tol:g}",
-                       "n": n, "m": m, "kkt_dim": N, "linear_solver": a.linear_solver, "solve_dim": NS,
-                       "batch_per_gpu": B, "global_batch": B * world,
-                       "sparsity": a.sparsity,
-                       "parallelism": f"dp{world} (instance shards, RCCL all-gather of results)" if distributed
-                       else "dp1"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "algorithmic_bytes": B * (8 * (n * n + m * n + m + n) + 8 * (n + 2 * m + 2) + 12),
-                         "kernel": "ipm_solve_kernel", "kernel_ms": kern_ms,
-                         "flops_per_launch": flops_launch,
-                         "executed_tflops": executed, "executed_frac": executed / FP64_PEAK_TFLOPS,
-                         "note": f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT "
-                                 f"system, 2N^3/3+2N^2 per Newton step) x the run's own Newton counts / "
-                                 f"HIP-event kernel time; executed_tflops counts what the kernel really does "
-                                 f"({a.linear_solver}: LU of dim {NS}" + (f" + 2n^2m Schur GEMM on fp64 MFMA"
-                                 if a.linear_solver == "schur" else "") + "); FP64 vector = matrix peak on MI355X"},
-            "newton_iters_mean": newton / (B * world),
-            "success_rate": solved,
-            "host_api_solves_per_s": host_rate,
+        full = gather.unpack([shard_range(pl["global_batch"], world, r)[1] for r in range(world)]
+                             if pl["scaling"] == "strong" else None)
+        assert int(full["status"].numel()) == pl["global_batch"], "gathered batch has the wrong size"
+        mine = full["status"][pl["start"]:pl["start"] + B].to(dev)
+        assert torch.equal(mine, out["status"]), "gathered results differ from this rank's"
+    if rank != 0:
+        return
+    G = pl["global_batch"]
+    ls = a.linear_solver
+    NS = solve_dim(n, m, ls)
+    cfg = {"mode": "c5" if a.sens else "c3", "n": n, "m": m, "batch_per_gpu": B, "linear_solver": ls,
+           "sparsity": a.sparsity}
+    key = f"{cfg['mode']}_n{n}_m{m}_b{B}_{ls}"
+    ev = evidence(key, cfg)
+    p = n * n + m * n + m + n
+    rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
+                  B * (8.0 * (p + n + 2 * m + 2) + 12.0), ev, "ipm_solve_kernel", roofline_bound(ls),
+                  f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system, 2N^3/3+2N^2 per "
+                  f"Newton step) x rank 0's own Newton counts / HIP-event time of the solve launch; executed = what "
+                  f"the kernel performs ({ls}: LU of dim {NS}" + (" + 2n^2m Schur GEMM on fp64 MFMA" if ls == "schur"
+                  else "") + "); bound: FP64 VALU issue (PMC, DESIGN.md §4); FP64 vector = matrix peak on MI355X; "
+                  "frac_trace: same FLOPs over the committed rocprofv3 trace of this configuration and build")
+    res = {
+        "metric": METRIC,
+        "value": a.steps * G / elapsed,
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": pl["scaling"],
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (random dense QPs of benchmark/quadratic_program_benchmark.jl, host numpy PCG64 in chunks "
+                f"of 4096 seeded SeedSequence({a.seed}, spawn_key=(chunk,)), uploaded to HBM before timing)",
+        "config": {"workload": (f"BASELINE {'C5' if a.sens else 'C3'}: random dense QP-KKT n={n} m={m} (KKT dim {N}), "
+                                f"fp64, global batch {G} ({B} on rank 0), tol={a.tol:g}"
+                                + (", solve + rrule pullback (VJP kernel) of f = Σx²+Σy²" if a.sens else "")),
+                   "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "solve_dim": NS,
+                   "batch_per_gpu": B, "global_batch": G, "sparsity": a.sparsity,
+                   "parallelism": f"dp{world} (instance shards, RCCL all-gather of results)" if distributed
+                   else "dp1"},
+        "roofline": rl,
+        "newton_iters_mean": newton_all / G,
+        "success_rate": solved_all / G,
+        "summary_statistics": summary_statistics(step_s, B, solved_all / G),
+        "host_api": host,
+        "evidence": evidence_id(key, cfg),
+    }
+    if a.sens:
+        vbytes = B * 8 * (2 * p + 3 * N + 2 * N)  # θ read, ∂θ written, (x,y,s) + cotangents read
+        vflops = B * lu_flops(N)
+        res["sensitivity"] = {
+            "vjp_kernel_ms": vjp_ms, "solve_kernel_ms": kern_ms, "vjp_per_s": B / (vjp_ms * 1e-3),
+            "vjp_failed": int((vstat != 0).sum().item()),
+            "vjp_roofline": {"flops_per_launch": vflops, "achieved_tflops": vflops / (vjp_ms * 1e-3) / 1e12,
+                             "frac_fp64": vflops / (vjp_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                             "algorithmic_bytes": vbytes, "achieved_gbs": vbytes / (vjp_ms * 1e-3) / 1e9,
+                             "frac_hbm": vbytes / (vjp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                             "note": "one dense LU of the N-dim ∇F_zᵀ (2N³/3+2N²) per instance; bytes = θ read + "
+                                     "∂θ written + z and cotangents"},
         }
-        if a.sens:
-            p = n * n + m * n + m + n
-            vbytes = B * 8 * (2 * p + 3 * N + 2 * N)  # θ read, ∂θ written, (x,y,s) + cotangents read
-            vflops = B * lu_flops(N)
-            res["config"]["workload"] = (f"BASELINE C5: batched solve + rrule pullback (VJP kernel) of f = Σx²+Σy², "
-                                         f"QP-KKT n={n} m={m} (KKT dim {N}), fp64, {B} instances per GPU, tol={a.tol:g}")
-            res["sensitivity"] = {
-                "vjp_kernel_ms": vjp_ms, "solve_kernel_ms": kern_ms,
-                "vjp_per_s": B / (vjp_ms * 1e-3),
-                "vjp_failed": int((vstat != 0).sum().item()),
-                "vjp_roofline": {"flops_per_launch": vflops, "achieved_tflops": vflops / (vjp_ms * 1e-3) / 1e12,
-                                 "frac_fp64": vflops / (vjp_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                                 "algorithmic_bytes": vbytes, "achieved_gbs": vbytes / (vjp_ms * 1e-3) / 1e9,
-                                 "frac_hbm": vbytes / (vjp_ms * 1e-3) / 8.0e12,
-                                 "note": "one dense LU of the N-dim ∇F_zᵀ (2N³/3+2N²) per instance; bytes = θ read + "
-                                         "∂θ written + z and cotangents"},
-            }
-        if world == 1 and a.cpu_sample > 0:
-            th = int(a.cpu_threads) or min(16, os.cpu_count() or 1)
-            res["cpu_baseline"] = cpu_baseline(theta_host[: a.cpu_sample], n, m, a.tol, th, a.linear_solver)
-        print(json.dumps(res), flush=True)
+    if world == 1 and a.cpu_sample != 0:
+        from oracle import coracle
+
+        coracle.build()
+        th = a.cpu_threads or host_cpus()["nproc"]
+        cb = cpu_baseline(lambda k, t: coracle.solve_batch(0, n, m, theta_host[:k], tol=a.tol, nthreads=t,
+                                                           linear_solver=ls),
+                          B, a, th, "C oracle (oracle/ipm_oracle.c, same algorithm and linear solver)")
+        r = cb.pop("_result")
+        cb["newton_mean"] = float(r["newton_iters"].mean())
+        res["cpu_baseline"] = cb
+    print(json.dumps(res), flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus > 1 and "RANK" not in os.environ:
+        return launch_ranks(a.gpus, os.path.abspath(__file__), argv)
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus > 1 and a.gpus != world:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if world > 1 and torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks but only {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+        return 2
+    distributed = world > 1 or (a.gather and "RANK" in os.environ)
     if distributed:
-        if a.gather and world == 1:  # rehearsal: the gathered batch must equal the local results
-            full = gather.unpack()
-            assert all(torch.equal(full[k], packed.views()[k].reshape(full[k].shape)) for k in full)
-        dist.destroy_process_group()
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("NCCL_DEBUG", "WARN")  # keep RCCL's banner off stdout (one JSON line)
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    pl = plan(a, world, rank)
+    try:
+        if a.lane_change:
+            main_lane_change(a, world, rank, local, dist, pl)
+        else:
+            main_qp(a, world, rank, local, dist, pl, distributed)
+    finally:
+        if distributed:
+            dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -11,6 +11,7 @@ the oracle.  hipcc cross-compiles for gfx950 without a GPU present.
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -36,11 +37,32 @@ FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off", "-f
          "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wall", "-Wno-unused-function", "-Wno-unused-result"]
 
 
+STAMP = LIB + ".srchash"
+
+
+def source_hash(extra_flags=()) -> str:
+    """sha256 over the text of every source the library is built from and the
+    compiler flags: the identity of a build (written next to the .so, quoted by
+    the profile summaries so that bench.py only cites evidence of this build)."""
+    h = hashlib.sha256()
+    for p in DEPS:
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0" + open(p, "rb").read() + b"\0")
+    h.update(" ".join([HIPCC.rsplit("/", 1)[-1], *FLAGS, *extra_flags]).encode())
+    return h.hexdigest()[:16]
+
+
+def built_hash() -> str | None:
+    """source_hash() recorded when mcp_amd/libmcpx.so was built, or None."""
+    try:
+        return open(STAMP).read().strip() or None
+    except OSError:
+        return None
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in DEPS)
+    # content, not mtimes: a snapshot copied to another machine keeps its stamp only
+    # if it was built from exactly these sources with these flags
+    return not os.path.exists(LIB) or built_hash() != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None) -> str:
@@ -77,6 +99,9 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     tmp = lib_path + ".tmp"
     subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], check=True)
     os.replace(tmp, lib_path)
+    if out is None:
+        with open(STAMP, "w") as f:
+            f.write(source_hash(extra_flags) + "\n")
     shutil.rmtree(tmp_dir, ignore_errors=True)
     if verbose:
         print(f"built {lib_path} in {time.time() - t0:.1f}s", flush=True)

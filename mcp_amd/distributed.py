@@ -9,6 +9,11 @@ record buffer (x | y | s | kkt_error | ϵ) and one int32 buffer
 (outer_iters | status | newton_iters), and two all-gathers (RCCL over xGMI with
 the "nccl" backend; gloo works the same way on CPU, which the tests use)
 deliver the whole batch to every rank.
+
+Shards may differ by one instance (``shard_range``: ⌊B/G⌋, +1 for the first
+B mod G ranks).  A collective needs equal buffer sizes, so every rank's packed
+buffers have room for ``capacity`` = ⌈B/G⌉ instances and the kernel writes
+the first ``B_rank`` of them; ``Gatherer.unpack`` drops each rank's padding.
 """
 
 from __future__ import annotations
@@ -24,37 +29,61 @@ def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
     return start, base + (1 if rank < extra else 0)
 
 
+def shard_capacity(total: int, world: int) -> int:
+    """Largest shard of `total` over `world` ranks, ⌈B/G⌉ (the common buffer size)."""
+    return -(-int(total) // int(world))
+
+
+_FP_FIELDS = (("x", "n"), ("y", "m"), ("s", "m"), ("kkt_error", 1), ("eps", 1))
+_INT_FIELDS = ("outer_iters", "status", "newton_iters")
+
+
 @dataclass
 class PackedResults:
-    """Per-instance outputs laid out for a single collective each."""
+    """Per-instance outputs laid out for a single collective each.
 
-    rec: "object"   # fp64 [B * (n + 2m + 2)]: x (B×n) | y (B×m) | s (B×m) | kkt (B) | ϵ (B)
-    irec: "object"  # int32 [3B]: outer_iters | status | newton_iters
+    Field blocks are `cap` instances long; the first `B` of each are this
+    rank's results (the rest is padding so that every rank's buffer has the
+    same size)."""
+
+    rec: "object"   # fp64 [cap * (n + 2m + 2)]: x (cap×n) | y (cap×m) | s (cap×m) | kkt (cap) | ϵ (cap)
+    irec: "object"  # int32 [3 cap]: outer_iters | status | newton_iters
     B: int
     n: int
     m: int
+    cap: int = -1
+
+    def __post_init__(self):
+        if self.cap < 0:
+            self.cap = self.B
+        if self.cap < self.B:
+            raise ValueError(f"capacity {self.cap} < batch {self.B}")
+
+    def _width(self, w) -> int:
+        return {"n": self.n, "m": self.m}.get(w, w)
 
     def views(self) -> dict:
         """Output dict (mcp_amd.batch layout) aliasing the packed buffers, so the
         kernel writes its results directly into them."""
-        B, n, m = self.B, self.n, self.m
+        B, cap = self.B, self.cap
         out, o = {}, 0
-        for k, w in (("x", n), ("y", m), ("s", m), ("kkt_error", 1), ("eps", 1)):
+        for k, w in _FP_FIELDS:
+            w = self._width(w)
             out[k] = self.rec[o:o + B * w].view(B, w) if k in ("x", "y", "s") else self.rec[o:o + B]
-            o += B * w
-        out["outer_iters"] = self.irec[:B]
-        out["status"] = self.irec[B:2 * B]
-        out["newton_iters"] = self.irec[2 * B:]
+            o += cap * w
+        for i, k in enumerate(_INT_FIELDS):
+            out[k] = self.irec[i * cap:i * cap + B]
         out["active_mask"] = None
         out["alpha_trace"] = None
         return out
 
 
-def alloc_packed(B: int, n: int, m: int, device) -> PackedResults:
+def alloc_packed(B: int, n: int, m: int, device, capacity: int | None = None) -> PackedResults:
     import torch
 
-    return PackedResults(torch.empty(B * (n + 2 * m + 2), dtype=torch.float64, device=device),
-                         torch.empty(3 * B, dtype=torch.int32, device=device), B, n, m)
+    cap = B if capacity is None else int(capacity)
+    return PackedResults(torch.empty(max(cap, 1) * (n + 2 * m + 2), dtype=torch.float64, device=device),
+                         torch.empty(3 * max(cap, 1), dtype=torch.int32, device=device), B, n, m, cap)
 
 
 class Gatherer:
@@ -82,19 +111,25 @@ class Gatherer:
             dist.all_gather(list(self.grec.chunk(self.world)), self.p.rec, group=self.group)
             dist.all_gather(list(self.girec.chunk(self.world)), self.p.irec, group=self.group)
 
-    def unpack(self) -> dict:
-        """Whole-batch results in global instance order (rank-major = shard order);
-        requires equal shard sizes (the weak-scaling benchmark)."""
+    def unpack(self, counts=None) -> dict:
+        """Whole-batch results in global instance order (rank-major = shard order).
+        `counts[r]` = instances rank r solved (default: every rank's B, the
+        equal-shard case); each rank's padding beyond its count is dropped."""
         import torch
 
-        B, n, m = self.p.B, self.p.n, self.p.m
+        cap, n, m = self.p.cap, self.p.n, self.p.m
+        counts = [self.p.B] * self.world if counts is None else [int(c) for c in counts]
+        if len(counts) != self.world or any(c < 0 or c > cap for c in counts):
+            raise ValueError(f"bad shard counts {counts} for capacity {cap} x {self.world} ranks")
         recs = self.grec.view(self.world, -1)
         irecs = self.girec.view(self.world, -1)
         out, o = {}, 0
-        for k, w in (("x", n), ("y", m), ("s", m), ("kkt_error", 1), ("eps", 1)):
-            part = recs[:, o:o + B * w]
-            out[k] = part.reshape(self.world * B, w) if k in ("x", "y", "s") else part.reshape(-1)
-            o += B * w
-        for i, k in enumerate(("outer_iters", "status", "newton_iters")):
-            out[k] = irecs[:, i * B:(i + 1) * B].reshape(-1)
-        return {k: torch.as_tensor(v) for k, v in out.items()}
+        for k, w in _FP_FIELDS:
+            w = self.p._width(w)
+            parts = [recs[r, o:o + counts[r] * w].reshape(counts[r], w) for r in range(self.world)]
+            cat = torch.cat(parts, 0)
+            out[k] = cat if k in ("x", "y", "s") else cat.reshape(-1)
+            o += cap * w
+        for i, k in enumerate(_INT_FIELDS):
+            out[k] = torch.cat([irecs[r, i * cap:i * cap + counts[r]] for r in range(self.world)])
+        return out

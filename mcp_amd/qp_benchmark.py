@@ -72,3 +72,35 @@ def generate_random_parameter_torch(generator, num_primals: int, num_inequalitie
     phi = torch.randn(B, n, **kw)
     return torch.cat([M.transpose(1, 2).reshape(B, n * n), A.transpose(1, 2).reshape(B, m * n),
                       b, phi], dim=1).contiguous()
+
+
+# Instances of a benchmark batch are drawn in fixed chunks, chunk c from its own
+# stream SeedSequence(seed, spawn_key=(c,)), so that instance i of the global batch
+# is the same whichever rank (and however many ranks) generates it: strong- and
+# weak-scaling runs at any GPU count solve identical θ.
+SEED_CHUNK = 4096
+
+
+def chunked_slice(draw, seed: int, start: int, count: int, chunk: int = SEED_CHUNK) -> np.ndarray:
+    """Rows [start, start + count) of a batch drawn chunk by chunk: `draw(rng, k)`
+    returns k rows, chunk c is drawn from SeedSequence(seed, spawn_key=(c,))."""
+    parts, i, end = [], int(start), int(start) + int(count)
+    while i < end:
+        c = i // chunk
+        block = draw(np.random.default_rng(np.random.SeedSequence(seed, spawn_key=(c,))), chunk)
+        lo, hi = i - c * chunk, min(end, (c + 1) * chunk) - c * chunk
+        parts.append(np.asarray(block)[lo:hi])
+        i += hi - lo
+    if not parts:
+        return np.empty((0, 0))
+    return np.ascontiguousarray(np.concatenate(parts, 0))
+
+
+def generate_global_slice(seed: int, num_primals: int, num_inequalities: int, sparsity_rate: float,
+                          start: int, count: int, chunk: int = SEED_CHUNK) -> np.ndarray:
+    """θ of global instances [start, start + count) of the QP batch seeded by `seed`."""
+    n, m = num_primals, num_inequalities
+    if count == 0:
+        return np.empty((0, theta_dim(n, m)))
+    return chunked_slice(lambda rng, k: generate_random_parameter(rng, n, m, sparsity_rate, batch=k),
+                         seed, start, count, chunk)

@@ -1,11 +1,14 @@
-"""bench.py helpers (CPU): FLOP accounting of SURVEY.md §8(d) and the committed
-PMC evidence the default bench line quotes as `roofline.traffic`."""
+"""bench.py helpers (CPU): FLOP accounting of SURVEY.md §8(d), the workload plan
+(strong / weak scaling), the rank launcher, the summary statistics of
+benchmark/path.jl and the rule that a bench line quotes rocprofv3 evidence only
+when it was taken on exactly its configuration and build."""
 
 import json
 import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -21,47 +24,121 @@ def test_lu_flops_matches_survey():
     assert round(bench.lu_flops(6)) == 216
 
 
-def test_solve_dims():
+def test_solve_dims_and_executed_flops():
     assert bench.solve_dim(32, 16, "dense") == 64
     assert bench.solve_dim(32, 16, "reduced") == 48
     assert bench.solve_dim(32, 16, "schur") == 32
+    assert bench.executed_flops(32, 16, "schur") == bench.lu_flops(32) + 2 * 32 * 32 * 16
+    assert bench.executed_flops(32, 16, "dense") == bench.lu_flops(64)
+    assert bench.roofline_bound("schur") == "valu"
 
 
-def test_pmc_summary_matches_default_config():
-    """The default bench line (C3, schur, 65,536 instances) must find its PMC summary;
-    other configurations must not borrow it."""
-    traffic, src = bench.pmc_traffic(32, 16, 65536, "schur")
-    d = json.load(open(os.path.join(ROOT, src)))
-    assert traffic == pytest.approx((d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0)
-    assert traffic > 0
-    assert bench.pmc_traffic(32, 16, 4096, "schur") == (None, None)
-    assert bench.pmc_traffic(16, 8, 65536, "schur") == (None, None)
-    assert bench.pmc_traffic(32, 16, 65536, "dense") == (None, None)
+def test_plan_strong_scaling_is_the_baseline_config():
+    """BASELINE C3: global 65,536 sharded over the GPUs (8,192 per GPU at N=8); C5: 4,096."""
+    a = bench.parse([])
+    assert bench.plan(a, 1, 0) == dict(start=0, count=65536, cap=65536, global_batch=65536, scaling="strong")
+    shards = [bench.plan(a, 8, r) for r in range(8)]
+    assert all(p["count"] == 8192 and p["cap"] == 8192 for p in shards)
+    assert [p["start"] for p in shards] == [8192 * r for r in range(8)]
+    assert bench.plan(bench.parse(["--sens"]), 8, 7)["count"] == 512
+    assert bench.plan(bench.parse(["--lane-change", "2"]), 1, 0)["count"] == 1024
+    ragged = [bench.plan(bench.parse(["--global-batch", "10"]), 4, r) for r in range(4)]
+    assert [p["count"] for p in ragged] == [3, 3, 2, 2] and all(p["cap"] == 3 for p in ragged)
+    weak = bench.plan(bench.parse(["--batch", "1000"]), 4, 3)
+    assert weak == dict(start=3000, count=1000, cap=1000, global_batch=4000, scaling="weak")
 
 
-def test_trace_summary_agrees_with_bench_events():
-    """profiles/r01: rocprofv3's average fast-pass duration and the bench's HIP-event
-    launch time (both passes) of the same command agree within 10 %."""
-    tr = json.load(open(os.path.join(ROOT, "profiles", "r01", "trace_c3_schur.json")))
-    b = json.load(open(os.path.join(ROOT, "profiles", "r01", "bench_c3_schur.json")))
-    assert tr["Grid_Size"] == 64 * b["config"]["batch_per_gpu"]
-    assert tr["avg_ms"] == pytest.approx(b["roofline"]["kernel_ms"], rel=0.10)
+def test_launcher_refuses_missing_gpus(capsys):
+    assert bench.launch_ranks(8, "unused.py", [], have_devices=1) == 2
+    assert "only 1 GPU" in capsys.readouterr().err
+
+
+@pytest.mark.slow
+def test_launch_ranks_spawns_world2(tmp_path):
+    """The `--gpus N` spawn path with world size 2 on CPU: torch.distributed.run as a
+    child, two ranks join a gloo group at 127.0.0.1 and shard the global batch."""
+    out = tmp_path / "ranks.json"
+    rc = bench.launch_ranks(2, os.path.join(ROOT, "tests", "helpers", "rank_probe.py"), [str(out), "65537"],
+                            have_devices=2)
+    assert rc == 0
+    d = json.load(open(out))
+    assert d["world"] == 2
+    assert d["shards"] == [[0, 0, 32769, 32769], [1, 32769, 32768, 32769]]
+
+
+def test_summary_statistics_format():
+    """benchmark/path.jl:101-126: success_rate, μ, σ of the runtimes."""
+    s = bench.summary_statistics([0.010, 0.012, 0.011], 1000, 0.95)["ip"]
+    assert s["success_rate"] == 0.95
+    assert s["μ"] == pytest.approx(1.1e-5)
+    assert s["σ"] == pytest.approx(np.std([1e-5, 1.2e-5, 1.1e-5], ddof=1))
+
+
+def test_evidence_only_for_its_config_and_build(tmp_path, monkeypatch):
+    from mcp_amd import build as b
+
+    monkeypatch.setattr(bench, "PROFILE_DIR", str(tmp_path))
+    monkeypatch.setattr(b, "built_hash", lambda: "abc")
+    cfg = {"mode": "c3", "n": 32, "m": 16, "batch_per_gpu": 65536, "linear_solver": "schur", "sparsity": 0.0}
+    json.dump({"config": cfg, "lib_hash": "abc", "FETCH_SIZE": 1000.0, "WRITE_SIZE": 24.0},
+              open(tmp_path / "pmc_x.json", "w"))
+    json.dump({"config": cfg, "lib_hash": "abc", "avg_ms": 6.0, "launch_avg_ms_all_passes": 6.01},
+              open(tmp_path / "trace_x.json", "w"))
+    ev = bench.evidence("x", cfg)
+    assert set(ev) == {"pmc", "trace"}
+    assert bench.pmc_traffic(ev)[0] == 1024.0 * 1024
+    r = bench.roofline(6.01, 78.6e9 * 6.01 * 0.5, 1e9, 1e9, ev, "k", "valu", "")
+    assert r["frac_trace"] == pytest.approx(0.5) and r["frac"] == pytest.approx(0.5)
+    assert bench.evidence("x", dict(cfg, batch_per_gpu=8192)) == {}  # another configuration
+    monkeypatch.setattr(b, "built_hash", lambda: "other")
+    assert bench.evidence("x", cfg) == {}  # another build of libmcpx.so
+
+
+def test_committed_evidence_is_self_consistent():
+    """Every committed profiles/r02 trace/PMC summary names its configuration and
+    build, and a bench line committed beside it quotes the same kernel time within 2 %."""
+    d = os.path.join(ROOT, "profiles", "r02")
+    if not os.path.isdir(d):
+        pytest.skip("no round-2 profiles yet")
+    for f in sorted(os.listdir(d)):
+        if f.startswith(("trace_", "pmc_")) and f.endswith(".json"):
+            j = json.load(open(os.path.join(d, f)))
+            assert "config" in j and "lib_hash" in j, f
+        if f.startswith("bench_") and f.endswith(".json"):
+            b = json.load(open(os.path.join(d, f)))
+            rl = b["roofline"]
+            if "frac_trace" in rl:
+                assert rl["frac_trace"] == pytest.approx(rl["frac"], rel=0.02), f
 
 
 def test_cli_has_every_baseline_mode():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], capture_output=True,
                          text=True, check=True).stdout
-    for flag in ("--gpus", "--steps", "--warmup", "--sens", "--lane-change", "--gather", "--cpu-sample"):
+    for flag in ("--gpus", "--steps", "--warmup", "--sens", "--lane-change", "--gather", "--cpu-sample",
+                 "--global-batch", "--batch", "--host-runs"):
         assert flag in out
 
 
 @pytest.mark.gpu
 def test_gpu_bench_lane_change_line():
     """The C4 bench line on a small batch: one JSON line, statuses equal to the C oracle's."""
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--lane-change", "2", "--batch", "64",
-                        "--steps", "1", "--warmup", "1", "--cpu-sample", "64"], capture_output=True, text=True,
-                       timeout=110, check=True)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--lane-change", "2", "--global-batch",
+                        "64", "--steps", "1", "--warmup", "1", "--cpu-sample", "64"], capture_output=True,
+                       text=True, timeout=110, check=True)
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["config"]["kkt_dim"] == 140 and d["n_gpus"] == 1
     assert d["value"] > 0 and 0 < d["roofline"]["frac"] < 1
     assert d["cpu_baseline"]["status_match"] is True
+
+
+@pytest.mark.gpu
+def test_gpu_bench_c3_small_line():
+    """The C3 line on a small global batch, with the host-API median and the CPU legs."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--global-batch", "2048", "--steps", "2",
+                        "--warmup", "1", "--cpu-sample", "256", "--host-runs", "2"], capture_output=True,
+                       text=True, timeout=110, check=True)
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["scaling"] == "strong" and d["config"]["global_batch"] == 2048
+    assert d["success_rate"] == 1.0 and d["host_api"]["median_solves_per_s"] > 0
+    assert d["cpu_baseline"]["cores"] == d["cpu_baseline"]["nproc"]
+    assert d["summary_statistics"]["ip"]["success_rate"] == 1.0
