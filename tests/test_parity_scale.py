@@ -1,0 +1,150 @@
+"""Parity pinned at scale, on the CPU (`-m "not gpu"`):
+
+* the shortcut linear solvers against the literal one.  The bench runs SCHUR
+  (slack and y blocks eliminated exactly, n×n Schur complement by pivot-free
+  Gauss-Jordan / pivoting LU); north_star names the dense LU with partial
+  pivoting of the full (n+2m)-dim ∇F + tol·I (src/solver.jl:81-83).  On the
+  bench's own C3 and C2 θ the two oracle modes agree on every discrete output
+  (status, outer / Newton counts, α-exponent traces, active sets) and on the
+  iterates to ≤1e-8.  On the 0.9-sparse stress set (mostly :failed instances)
+  rounding-level differences change some failed trajectories; those
+  divergences are recorded here exactly;
+* the ϵ-continuation factors 1 − exp(−0.1k) and 1 + exp(−0.5k)
+  (src/solver.jl:111-113), which host libm tabulates for oracle and kernel
+  alike, against correctly rounded values (mpmath at 200 bits);
+* the generated nonlinear code (mcp_amd/codegen.py, compiled from the same text
+  for the GPU and the oracle) against central finite differences of the host F
+  (sympy-lambdified G, H of the lane-change game, src/mcp.jl:72-120).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from mcp_amd.qp_benchmark import generate_global_slice
+
+TRACE = 1024  # ≥ 931 = 49 × 19, the longest possible solve
+
+
+def _solve_both(coracle, n, m, theta):
+    return {ls: coracle.solve_batch(0, n, m, theta, tol=1e-6, linear_solver=ls, nthreads=8, trace_len=TRACE)
+            for ls in ("schur", "dense")}
+
+
+def _z(r):
+    return np.concatenate([r["x"], r["y"], r["s"]], 1)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n,m,B", [(32, 16, 8192), (16, 8, 4096)], ids=["C3_8192", "C2_4096"])
+def test_schur_equals_full_lu_on_bench_inputs(oracle_lib, n, m, B):
+    """bench.py's θ (seed 1, instances 0..B−1): SCHUR ≡ dense full-system LU."""
+    th = generate_global_slice(1, n, m, 0.0, 0, B)
+    r = _solve_both(oracle_lib, n, m, th)
+    a, d = r["schur"], r["dense"]
+    for k in ("status", "outer_iters", "newton_iters", "active_mask", "alpha_trace"):
+        assert np.array_equal(a[k], d[k]), k
+    assert np.all(a["status"] == 0)
+    rel = np.abs(_z(a) - _z(d)).max(1) / np.maximum(1.0, np.abs(_z(d)).max(1))
+    assert rel.max() <= 1e-8
+    for k in ("kkt_error", "eps"):
+        assert np.all(np.abs(a[k] - d[k]) <= 1e-8 * np.maximum(1.0, np.abs(d[k])))
+
+
+@pytest.mark.slow
+def test_sparse_stress_set_divergences_are_recorded(oracle_lib):
+    """0.9-sparse QPs (the reference benchmark's default sparsity), 512 instances:
+    only 10 are :solved under either solver.  The two exact eliminations differ in
+    rounding, which moves some failing trajectories: 9 Newton counts, 10 α traces
+    and 1 final active set differ — never a status, never a solved instance."""
+    th = generate_global_slice(1, 16, 8, 0.9, 0, 512)
+    r = _solve_both(oracle_lib, 16, 8, th)
+    a, d = r["schur"], r["dense"]
+    assert np.array_equal(a["status"], d["status"])
+    assert int((a["status"] == 0).sum()) == 10
+    newton = a["newton_iters"] != d["newton_iters"]
+    alpha = (a["alpha_trace"] != d["alpha_trace"]).any(axis=(1, 2))
+    active = (a["active_mask"] != d["active_mask"]).any(axis=1)
+    assert (int(newton.sum()), int(alpha.sum()), int(active.sum())) == (9, 10, 1)
+    diverged = newton | alpha | active | (a["outer_iters"] != d["outer_iters"])
+    assert np.all(a["status"][diverged] == 1)
+    ok = a["status"] == 0
+    assert np.abs(_z(a)[ok] - _z(d)[ok]).max() <= 1e-8 * max(1.0, np.abs(_z(d)[ok]).max())
+
+
+class _Tables(C.Structure):  # oracle_tables of oracle/ipm_oracle.c
+    _fields_ = [("alpha", C.c_double * 64), ("n_trials", C.c_int), ("c_tau", C.c_double),
+                ("tight", C.c_double * 129), ("loose", C.c_double * 129)]
+
+
+def test_eps_tables_are_correctly_rounded(oracle_lib):
+    """src/solver.jl:111-113 factors as tabulated by libm for k = 0..128 (rates 0.1 and
+    0.5, the defaults): exp(−r·k) correctly rounded, then the fp64 1 ∓ e."""
+    mpmath = pytest.importorskip("mpmath")
+    from mcp_amd._abi import make_params
+
+    t = _Tables()
+    prm = make_params(max_inner_iters=128)
+    L = oracle_lib.lib()
+    L.oracle_build_tables.argtypes = [C.c_void_p, C.POINTER(_Tables)]
+    assert L.oracle_build_tables(C.byref(prm), C.byref(t)) == 0
+    mpmath.mp.prec = 200
+    for k in range(129):
+        for rate, table, sign in ((0.1, t.tight, -1.0), (0.5, t.loose, 1.0)):
+            arg = -rate * float(k)  # the fp64 product the reference and the tables form
+            e = float(mpmath.exp(mpmath.mpf(arg)))  # mpf → float rounds to nearest
+            want = 1.0 + sign * e
+            assert table[k] == want, (rate, k, table[k], want)
+
+
+@pytest.mark.slow
+def test_lane_change_generated_jacobian_matches_finite_differences(oracle_lib):
+    """The generated ∇F_z blocks P = ∂G/∂x, Q = ∂G/∂y, R = ∂H/∂x (the code the gfx950
+    module runs, here compiled by gcc) against central differences of the host F
+    (lambdified G, H: an evaluation path that shares no code with codegen's
+    printer), and the generated G, H against the host F, at random z."""
+    from mcp_amd.lane_change import LaneChangeGame
+
+    game = LaneChangeGame(2)
+    mcp = game.mcp
+    nl = mcp.nl
+    n, m = nl.n, nl.m
+    G = oracle_lib.nl_lib(nl)
+    G.oracle_nl_init.argtypes = [C.c_void_p, C.c_void_p]
+    G.oracle_nl_eval.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    rng = np.random.default_rng(7)
+    thetas = mcp.theta_map(game.generate_random_parameter(rng, 3))
+    for th in thetas:
+        th = np.ascontiguousarray(th)
+        x = rng.standard_normal(n)
+        y = rng.uniform(0.1, 2.0, m)
+        s = rng.uniform(0.1, 2.0, m)
+        blk = np.zeros(nl.size + 1)
+        z = np.ascontiguousarray(np.concatenate([x, y]))
+        G.oracle_nl_init(th.ctypes.data, blk.ctypes.data)
+        G.oracle_nl_eval(th.ctypes.data, z.ctypes.data, blk.ctypes.data)
+        P = blk[nl.OFF_P:nl.OFF_Q].reshape(n, n, order="F")
+        Q = blk[nl.OFF_Q:nl.OFF_R].reshape(m, n).T          # Q[i, k] = blk[OFF_Q + k·n + i]
+        R = blk[nl.OFF_R:nl.OFF_G].reshape(n, m).T          # R[k, j] = blk[OFF_R + j·m + k]
+        g, h = blk[nl.OFF_G:nl.OFF_H], blk[nl.OFF_H:nl.OFF_H + m]
+        F0 = mcp.F(x, y, s, θ=th, ϵ=0.0)
+        np.testing.assert_allclose(g, F0[:n], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(h - s, F0[n:n + m], rtol=1e-12, atol=1e-12)
+        J = np.zeros((n + m, n + m))
+        hstep = 1e-6
+        for j in range(n + m):
+            e = np.zeros(n + m)
+            e[j] = hstep
+            zp, zm = z + e, z - e
+            Fp = mcp.F(zp[:n], zp[n:], s, θ=th, ϵ=0.0)
+            Fm = mcp.F(zm[:n], zm[n:], s, θ=th, ϵ=0.0)
+            J[:, j] = (Fp[:n + m] - Fm[:n + m]) / (2 * hstep)
+        # G and H are at most quadratic in z: central differences are exact up to rounding
+        scale = max(1.0, np.abs(J).max())
+        np.testing.assert_allclose(P, J[:n, :n], atol=1e-7 * scale)
+        np.testing.assert_allclose(Q, J[:n, n:], atol=1e-7 * scale)
+        np.testing.assert_allclose(R, J[n:, :n], atol=1e-7 * scale)
+        assert not nl.has_s and np.abs(J[n:, n:]).max() <= 1e-7 * scale  # ∂H/∂y ≡ 0 (SCHUR applies)
