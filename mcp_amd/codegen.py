@@ -57,6 +57,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
 GEN_VERSION = 2
+_MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function")
+_MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "../../include/mcpx.h")
 LDS_LIMIT = 160 * 1024 - 2048  # bytes of static LDS one workgroup may declare on gfx950 (minus headroom)
 
 _FUNCS = {  # sympy function → C name (both libm and HIP device math)
@@ -278,8 +280,18 @@ class NLSystem:
             "",
         ])
 
+    def module_key(self) -> str:
+        """Content hash of everything the code object is built from: the generated
+        text, the kernel headers it includes and the compiler flags (self.key, the
+        oracle's cache key, covers the generated text only)."""
+        h = hashlib.sha256(self.key.encode())
+        for f in _MODULE_DEPS:
+            h.update(f.encode() + b"\0" + open(os.path.join(CSRC, f), "rb").read())
+        h.update(" ".join(_MODULE_FLAGS).encode())
+        return h.hexdigest()[:24]
+
     def module_path(self) -> str:
-        return os.path.join(GEN_DIR, f"nl_{self.key}.hsaco")
+        return os.path.join(GEN_DIR, f"nl_{self.module_key()}.hsaco")
 
     def build_module(self, verbose: bool = False) -> str:
         """Compile (or reuse, by content hash) the gfx950 code object; returns its path."""
@@ -287,13 +299,12 @@ class NLSystem:
         if os.path.exists(path):
             return path
         os.makedirs(GEN_DIR, exist_ok=True)
-        src = os.path.join(GEN_DIR, f"nl_{self.key}.hip")
+        src = os.path.join(GEN_DIR, f"nl_{self.module_key()}.hip")
         with open(src, "w") as f:
             f.write(self.hip_source())
         tmp_dir = tempfile.mkdtemp(prefix="mcpx_gen_")
         tmp = os.path.join(tmp_dir, os.path.basename(path))
-        cmd = [HIPCC, "--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off",
-               "-Wno-unused-function", "-I", CSRC, "-save-temps", "-o", tmp, src]
+        cmd = [HIPCC, *_MODULE_FLAGS, "-I", CSRC, "-save-temps", "-o", tmp, src]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True, cwd=tmp_dir)

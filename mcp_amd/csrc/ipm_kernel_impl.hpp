@@ -253,11 +253,20 @@ __device__ __forceinline__ void assemble_row(const double* __restrict__ th, cons
   }
 }
 
-// a[j] ← fma(−l, u_j, a[j]) for j in (k, NMAX) and rhs ← fma(−l, u_rhs, rhs),
-// where u is the row held by the lane(s) in `pm`, broadcast through SGPRs in
-// groups of ≤16 columns (bcast_group.inc).
+// a[j] ← fma(−l, u_j, a[j]) for j in (k, NMAX) and rhs ← fma(−l, u_rhs, rhs) in
+// the lanes where `upd` holds, where u is the row held by the lane in `pm`,
+// broadcast through SGPRs in groups of ≤16 columns (bcast_group.inc).
+//
+// The broadcast runs in uniform control flow (full EXEC) and only the fmas are
+// predicated.  The asm switches EXEC to the pivot lane and reads its VGPRs; the
+// pivot lane is never among the updated lanes, so under a compiler-narrowed EXEC
+// any copy the compiler places into the asm's input registers (a reload of a
+// spilled a[j] from an AGPR, a register move) would skip the pivot lane and the
+// asm would broadcast a stale value.  That is what the ×5-unrolled C4 Schur
+// formation did; tools/check_dpp_hazards.py rejects the pattern.
 template <int NMAX>
-__device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, int k, double l, uint64_t pm) {
+__device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, int k, double l, uint64_t pm,
+                                              bool upd) {
   constexpr int G = 16;  // columns per EXEC-masked broadcast
   // columns k+1 .. NMAX-1 and the right-hand side (index NMAX)
 #pragma clang loop unroll(full)
@@ -273,11 +282,13 @@ __device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, in
       v[t] = (t < cnt) ? ((j < NMAX) ? a[j < NMAX ? j : 0] : rhs) : 0.0;
     }
     bcast_n(cnt, v, pm, u);
+    if (upd) {
 #pragma clang loop unroll(full)
-    for (int t = 0; t < 16; ++t) {
-      const int j = lo + t;
-      if (t < cnt && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
-      if (t < cnt && j == NMAX) rhs = fma(-l, u[t], rhs);
+      for (int t = 0; t < 16; ++t) {
+        const int j = lo + t;
+        if (t < cnt && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
+        if (t < cnt && j == NMAX) rhs = fma(-l, u[t], rhs);
+      }
     }
   }
 }
@@ -307,11 +318,8 @@ __device__ __forceinline__ bool gj_spd_rows(double (&a)[NMAX], double& rhs, int 
     // its store→load→fma latency chain per step measured 1.45× slower at C3.
     // The mask is re-materialised per step (opaque): hoisted, the 32 constant
     // masks would occupy 64 SGPRs and spill.
-    if (ln == k) {
-      dg = piv;
-    } else {
-      eliminate_row<NMAX>(a, rhs, k, a[k] / piv, (uint64_t)opaque64((int64_t)(1ull << k)));
-    }
+    if (ln == k) dg = piv;
+    eliminate_row<NMAX>(a, rhs, k, a[k] / piv, (uint64_t)opaque64((int64_t)(1ull << k)), ln != k);
   }
   if (!ok) return false;
   dz = rhs / dg;
@@ -357,7 +365,7 @@ __device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int
     rem &= ~(1ull << p);
     if (ln == p) my_step = k;
     if (ln == k) pk = p;
-    if ((rem >> ln) & 1ull) eliminate_row<NMAX>(a, rhs, k, ak / piv, 1ull << p);
+    eliminate_row<NMAX>(a, rhs, k, ak / piv, 1ull << p, (rem >> ln) & 1ull);
   }
   if (singular) return false;
   dz = 0.0;

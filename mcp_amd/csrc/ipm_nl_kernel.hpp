@@ -148,7 +148,9 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
         }
         double rhs = lx ? -Fs[i] : 0.0;
         // unrolled ×2 so the uniform R·D⁻¹ row loads of k+1 overlap the fmas of k (same fma
-        // order per a[j]); C4: 13 % less time per Newton step.  ×5 spills into AGPRs.
+        // order per a[j]); C4: 13 % less time per Newton step.  ×5 keeps part of a[] in AGPRs
+        // and runs 29 % slower (it returned wrong iterates before the broadcast left the
+        // divergent region).
 #pragma unroll 2
         for (int k = 0; k < m; ++k) {
           const double q = lx ? -blk[OFF_Q + k * n + i] : 0.0;

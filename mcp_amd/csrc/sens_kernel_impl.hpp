@@ -134,11 +134,12 @@ __device__ __forceinline__ double dtheta_row(const double* __restrict__ d, const
   return 0.0;
 }
 
-// a[j] ← fma(−l, u_j, a[j]) for j in (k, NMAX) and r[c] ← fma(−l, u_{NMAX+c}, r[c]):
-// eliminate_row() of the solver, widened to R right-hand sides.
+// a[j] ← fma(−l, u_j, a[j]) for j in (k, NMAX) and r[c] ← fma(−l, u_{NMAX+c}, r[c])
+// in the lanes where `upd` holds: eliminate_row() of the solver, widened to R
+// right-hand sides (broadcast at full EXEC, only the fmas predicated — see there).
 template <int NMAX, int R>
 __device__ __forceinline__ void eliminate_row_multi(double (&a)[NMAX], double (&r)[R], int k, double l,
-                                                    uint64_t pm) {
+                                                    uint64_t pm, bool upd) {
   constexpr int G = 16;
   constexpr int W = NMAX + R;
 #pragma clang loop unroll(full)
@@ -154,11 +155,13 @@ __device__ __forceinline__ void eliminate_row_multi(double (&a)[NMAX], double (&
       v[t] = (t < cnt) ? ((j < NMAX) ? a[j < NMAX ? j : 0] : r[j >= NMAX && j - NMAX < R ? j - NMAX : 0]) : 0.0;
     }
     bcast_n(cnt, v, pm, u);
+    if (upd) {
 #pragma clang loop unroll(full)
-    for (int t = 0; t < 16; ++t) {
-      const int j = lo + t;
-      if (t < cnt && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
-      if (t < cnt && j >= NMAX) r[j - NMAX < R ? j - NMAX : 0] = fma(-l, u[t], r[j - NMAX < R ? j - NMAX : 0]);
+      for (int t = 0; t < 16; ++t) {
+        const int j = lo + t;
+        if (t < cnt && j < NMAX) a[j < NMAX ? j : 0] = fma(-l, u[t], a[j < NMAX ? j : 0]);
+        if (t < cnt && j >= NMAX) r[j - NMAX < R ? j - NMAX : 0] = fma(-l, u[t], r[j - NMAX < R ? j - NMAX : 0]);
+      }
     }
   }
 }
@@ -202,7 +205,7 @@ __device__ __forceinline__ bool lu_solve_rows_multi(double (&a)[NMAX], double (&
     rem &= ~(1ull << p);
     if (ln == p) my_step = k;
     if (ln == k) pk = p;
-    if ((rem >> ln) & 1ull) eliminate_row_multi<NMAX, R>(a, r, k, ak / piv, 1ull << p);
+    eliminate_row_multi<NMAX, R>(a, r, k, ak / piv, 1ull << p, (rem >> ln) & 1ull);
   }
   if (singular) return false;
 #pragma unroll

@@ -1,13 +1,28 @@
-"""Static check of VALU-write → cross-lane-read hazards around the inline asm.
+"""Static checks of the inline asm's cross-lane reads in a gfx950 .s (-save-temps).
 
-A DPP instruction reading a VGPR that a VALU instruction wrote fewer than 2 wait
-states earlier reads a stale value (gfx9 hazard table; hipcc does not pad
-hazards whose consumer sits inside an asm statement).  Scans the .s of a
--save-temps build: for every *_dpp instruction, walks back through the
-preceding instructions counting wait states (an instruction = 1, s_nop N = N+1)
-and flags a VALU write to the DPP source register (src0) within 2 states.
+1. Wait states.  A DPP instruction reading a VGPR that a VALU instruction wrote
+   fewer than 2 wait states earlier reads a stale value (gfx9 hazard table);
+   v_readlane / v_readfirstlane need 1, v_permlane*_swap 2.  hipcc does not pad
+   hazards whose consumer sits inside an asm statement.  For every such reader,
+   walk back through the preceding instructions counting wait states (an
+   instruction = 1, s_nop N = N+1) and flag a VALU write to its source.
+
+2. EXEC-switched broadcasts under a compiler-narrowed EXEC.  The broadcast asm
+   (csrc/bcast_group.inc) saves EXEC, sets it to the pivot lane and reads that
+   lane's VGPRs with v_readfirstlane.  If the asm sits inside a divergent region
+   (after s_and_saveexec_b64 & co. without the matching restore), the pivot lane
+   is typically inactive there, and any copy the compiler places into the asm's
+   input registers inside the region — a reload of a spilled value from an AGPR,
+   a register move — skips that lane: the asm then broadcasts a stale value.
+   This is how the ×5-unrolled C4 Schur formation returned wrong iterates
+   (DESIGN.md §4).  The kernels broadcast in uniform control flow; every
+   EXEC-switching asm block is walked back along its fall-through path to the
+   nearest label / unconditional branch / EXEC restore, and an EXEC narrowing met
+   first is a hazard (the number of source registers redefined in between is
+   reported).
 
     python tools/check_dpp_hazards.py path/to/file.s [kernel-substring]
+Exit status 1 if any hazard is found.
 """
 
 from __future__ import annotations
@@ -16,6 +31,8 @@ import re
 import sys
 
 REG = re.compile(r"v\[(\d+):(\d+)\]|v(\d+)")
+NARROW = ("s_and_saveexec_b64", "s_andn2_saveexec_b64", "s_and_saveexec_b32")
+EXEC_WRITES = ("s_and_b64", "s_andn2_b64", "s_xor_b64", "s_or_b64", "s_mov_b64", "s_cselect_b64")
 
 
 def regs(tok: str) -> set:
@@ -28,31 +45,42 @@ def regs(tok: str) -> set:
     return out
 
 
-def main():
-    path = sys.argv[1]
-    want = sys.argv[2] if len(sys.argv) > 2 else ""
-    lines = open(path).read().split("\n")
+def parse(path: str):
+    """[(kernel, text, in_asm, is_label)] in file order."""
     kernel = None
-    insts = []  # (kernel, text, in_asm)
+    out = []
     in_asm = False
-    for l in lines:
+    for l in open(path).read().split("\n"):
         if ";;#ASMSTART" in l:
             in_asm = True
         if ";;#ASMEND" in l:
             in_asm = False
         t = l.split(";")[0].strip()
-        if t.endswith(":") and not t.startswith(".") and "_Z" in t:
+        if t.endswith(":") and not t.startswith(".") and ("_Z" in t or "mcpx" in t):
             kernel = t[:-1]
+            continue
+        if t.endswith(":") and t.startswith(".LBB"):
+            out.append((kernel, t, in_asm, True))
             continue
         if not t or t.startswith(".") or t.endswith(":"):
             continue
-        insts.append((kernel, t, in_asm))
-    bad = 0
-    checked = 0
-    for i, (k, t, asm) in enumerate(insts):
-        op = t.split()[0]
-        if want and want not in (k or ""):
+        out.append((kernel, t, in_asm, False))
+    return out
+
+
+def valu_dst(t: str) -> set:
+    o = t.split()[0]
+    if o.startswith("v_") and not o.startswith(("v_readfirstlane", "v_readlane", "v_cmp")):
+        return regs(t[len(o):].split(",")[0])
+    return set()
+
+
+def wait_state_hazards(insts, want: str):
+    bad, checked = [], 0
+    for i, (k, t, asm, lab) in enumerate(insts):
+        if lab or (want and want not in (k or "")):
             continue
+        op = t.split()[0]
         ops = [x.strip() for x in t[len(op):].split(",")]
         if "_dpp" in op and len(ops) >= 2:
             src, need = regs(ops[1]), 2          # VALU write → DPP read: 2 wait states
@@ -66,24 +94,83 @@ def main():
         states = 0
         j = i - 1
         while j >= 0 and states < need:
-            kk, tt, _ = insts[j]
+            kk, tt, _, ll = insts[j]
             if kk != k:
                 break
+            if ll:
+                j -= 1
+                continue
             o = tt.split()[0]
             if o == "s_nop":
                 states += int(tt.split()[1], 0) + 1
                 j -= 1
                 continue
-            if o.startswith("v_") and not o.startswith("v_readfirstlane") and not o.startswith("v_readlane") \
-                    and not o.startswith("v_cmp"):
-                dst = regs(tt[len(o):].split(",")[0])
-                if dst & src:
-                    bad += 1
-                    print(f"HAZARD in {k}:\n   {tt}\n   {t}  ({states} wait states between)")
+            if valu_dst(tt) & src:
+                bad.append(f"WAIT-STATE HAZARD in {k}:\n   {tt}\n   {t}  ({states} wait states between)")
             states += 1
             j -= 1
-    print(f"checked {checked} DPP / asm cross-lane instructions, {bad} hazards")
-    return 1 if bad else 0
+    return bad, checked
+
+
+def exec_switch_blocks(insts):
+    """Start indices of asm blocks that save EXEC and set it (s_mov_b64 sX, exec;
+    s_mov_b64 exec, sY), with the VGPRs their v_readfirstlane read."""
+    for i, (k, t, asm, lab) in enumerate(insts):
+        if not asm or lab or i + 1 >= len(insts):
+            continue
+        if re.fullmatch(r"s_mov_b64\s+s\[\d+:\d+\],\s*exec", t) and insts[i + 1][1].startswith("s_mov_b64 exec"):
+            src, j = set(), i + 2
+            while j < len(insts) and insts[j][2] and not insts[j][1].startswith("s_mov_b64 exec"):
+                if insts[j][1].startswith("v_readfirstlane"):
+                    src |= regs(insts[j][1].split(",", 1)[1])
+                j += 1
+            yield i, src
+
+
+def narrowed_exec_hazards(insts, want: str):
+    bad, checked = [], 0
+    for i, src in exec_switch_blocks(insts):
+        k = insts[i][0]
+        if want and want not in (k or ""):
+            continue
+        checked += 1
+        redefined = set()
+        j = i - 1
+        while j >= 0:
+            kk, tt, asm, lab = insts[j]
+            if kk != k or lab:
+                break  # a join point / another function: not this path's business
+            o = tt.split()[0]
+            if not asm:
+                if o in ("s_branch", "s_setpc_b64", "s_endpgm"):
+                    break  # not a fall-through predecessor
+                if o in NARROW or (o in EXEC_WRITES and re.match(r"\S+\s+exec,", tt) and o != "s_or_b64"
+                                   and not (o == "s_mov_b64" and "exec, -1" in tt)):
+                    bad.append(f"NARROWED-EXEC BROADCAST in {k}: the asm block at instruction {i} switches EXEC "
+                               f"inside a divergent region opened by `{tt}`; {len(redefined & src)} of its "
+                               f"{len(src)} source VGPRs redefined in between")
+                    break
+                if o == "s_or_b64" and re.match(r"s_or_b64\s+exec,", tt) or (o == "s_mov_b64" and "exec, -1" in tt):
+                    break  # EXEC restored on this path
+                if o.startswith("s_or_saveexec"):
+                    break
+            redefined |= valu_dst(tt)
+            j -= 1
+    return bad, checked
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    path = argv[0]
+    want = argv[1] if len(argv) > 1 else ""
+    insts = parse(path)
+    w, wc = wait_state_hazards(insts, want)
+    x, xc = narrowed_exec_hazards(insts, want)
+    for msg in (w + x)[:50]:
+        print(msg)
+    print(f"checked {wc} DPP / asm cross-lane instructions and {xc} EXEC-switched broadcasts: "
+          f"{len(w)} wait-state hazards, {len(x)} narrowed-EXEC broadcasts")
+    return 1 if (w or x) else 0
 
 
 if __name__ == "__main__":
