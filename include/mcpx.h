@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define MCPX_VERSION 10200 /* 1.2.0 */
+#define MCPX_VERSION 10300 /* 1.3.0 */
 
 /* error codes */
 #define MCPX_OK 0
@@ -69,9 +69,24 @@ extern "C" {
 #define MCPX_FAMILY_AFFINE 1
 #define MCPX_FAMILY_NONLINEAR 2
 
-/* largest linear-system dimension of the register-resident kernels
+/* largest linear-system dimension of the register-resident one-wave kernels
  * (n + m for MCPX_LINSOLVE_REDUCED, n + 2m for MCPX_LINSOLVE_DENSE) */
 #define MCPX_MAX_KKT_DIM 64
+/* largest KKT dimension n + 2m of the workgroup-per-instance kernels of the QP
+ * and affine families (blocked LU with MFMA trailing updates, REDUCED / DENSE);
+ * a generated nonlinear module sizes its own (mcpx_module_dims) */
+#define MCPX_MAX_WG_KKT_DIM 768
+
+/* Which kernel family runs a solve (mcpx_params.kernel):
+ *  MCPX_KERNEL_AUTO       one wave per instance when the system fits its 64 rows,
+ *                         else one workgroup per instance;
+ *  MCPX_KERNEL_WAVE       only the one-wave kernels (MCPX_EUNSUPPORTED beyond);
+ *  MCPX_KERNEL_WORKGROUP  the workgroup-per-instance kernels at any size they
+ *                         support (REDUCED / DENSE, and SCHUR for generated
+ *                         modules) — bit-identical results to the one-wave path. */
+#define MCPX_KERNEL_AUTO 0
+#define MCPX_KERNEL_WAVE 1
+#define MCPX_KERNEL_WORKGROUP 2
 /* largest max_inner_iters (ϵ-schedule table length) */
 #define MCPX_MAX_INNER_ITERS 128
 /* largest number of line-search trials (α = decayᵉ, e = 0..E) */
@@ -107,7 +122,7 @@ typedef struct mcpx_params {
   int32_t max_inner_iters;  /* 20 */
   int32_t max_outer_iters;  /* 50 */
   int32_t linear_solver;    /* MCPX_LINSOLVE_* — the reference's linear_solve_algorithm kwarg (src/solver.jl:50) */
-  int32_t pad_;
+  int32_t kernel;           /* MCPX_KERNEL_* (0 = auto) */
 } mcpx_params;
 
 /* Batch descriptor. */
@@ -220,15 +235,19 @@ int mcpx_jvp_batch_device(const mcpx_desc* desc, const double* theta, const doub
  * Jacobian blocks, compiled with the solver template
  * (mcp_amd/csrc/ipm_nl_kernel.hpp) into one gfx950 code object per problem.
  * These calls load and run it.  A module holds the kernels its size admits:
- * MCPX_LINSOLVE_SCHUR (∂H/∂y ≡ 0, n ≤ 64, m ≤ 128), _REDUCED (n + m ≤ 64),
- * _DENSE (n + 2m ≤ 64); another linear_solver is MCPX_EUNSUPPORTED.
+ * one-wave MCPX_LINSOLVE_SCHUR (∂H/∂y ≡ 0, n ≤ 64, m ≤ 128), _REDUCED
+ * (n + m ≤ 64), _DENSE (n + 2m ≤ 64), and workgroup-per-instance kernels of
+ * each of them (SCHUR: ∂H/∂y ≡ 0) whose LDS footprint fits
+ * (e.g. the lane change at T = 10: n = 200, m = 250, KKT dimension 700);
+ * another linear_solver is MCPX_EUNSUPPORTED.
  */
 typedef struct mcpx_module mcpx_module;
 /* Loads the code object at `path` on the current device (other devices load
  * it on first use).  No usable GPU: MCPX_ENODEV. */
 int mcpx_module_load(const char* path, mcpx_module** mod);
-/* The module's n, m, θ dimension p and kernel mask (bit MCPX_LINSOLVE_*);
- * NULL pointers are skipped. */
+/* The module's n, m, θ dimension p and kernel mask: bit MCPX_LINSOLVE_* for the
+ * one-wave kernels, bit 3 + MCPX_LINSOLVE_* for the workgroup kernels; NULL
+ * pointers are skipped. */
 int mcpx_module_dims(const mcpx_module* mod, int32_t* n, int32_t* m, int32_t* p, int32_t* solvers);
 void mcpx_module_unload(mcpx_module* mod);
 /* mcpx_solve_batch / mcpx_solve_batch_device for the module's problem:

@@ -16,6 +16,9 @@ FAMILY_AFFINE = 1
 FAMILY_NONLINEAR = 2  # generated device code per problem (mcp_amd/codegen.py)
 
 MAX_KKT_DIM = 64
+MAX_WG_KKT_DIM = 768  # MCPX_MAX_WG_KKT_DIM: workgroup-per-instance kernels (QP / affine)
+KERNEL_AUTO, KERNEL_WAVE, KERNEL_WORKGROUP = 0, 1, 2
+KERNELS = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "workgroup": KERNEL_WORKGROUP}
 JVP_RHS = 8  # MCPX_JVP_RHS: partials per factorisation of the JVP kernel
 
 LINSOLVE_REDUCED = 0
@@ -46,7 +49,7 @@ class Params(C.Structure):
         ("max_inner_iters", C.c_int32),
         ("max_outer_iters", C.c_int32),
         ("linear_solver", C.c_int32),
-        ("pad_", C.c_int32),
+        ("kernel", C.c_int32),
     ]
 
 
@@ -80,12 +83,14 @@ class Out(C.Structure):
 
 def make_params(tol=1e-4, max_inner_iters=20, max_outer_iters=50, tightening_rate=0.1,
                 loosening_rate=0.5, min_stepsize=1e-4, tau=0.995, decay=0.5,
-                linear_solver="reduced") -> Params:
+                linear_solver="reduced", kernel="auto") -> Params:
     """Defaults exactly as src/solver.jl:42-48 and :127.  `linear_solver` plays the
-    role of the reference's `linear_solve_algorithm` kwarg (src/solver.jl:50)."""
+    role of the reference's `linear_solve_algorithm` kwarg (src/solver.jl:50);
+    `kernel` picks the one-wave or the workgroup-per-instance kernels (MCPX_KERNEL_*)."""
     ls = LINEAR_SOLVERS[linear_solver] if isinstance(linear_solver, str) else int(linear_solver)
+    kk = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
     return Params(float(tol), float(tightening_rate), float(loosening_rate), float(min_stepsize),
-                  float(tau), float(decay), int(max_inner_iters), int(max_outer_iters), ls, 0)
+                  float(tau), float(decay), int(max_inner_iters), int(max_outer_iters), ls, kk)
 
 
 def theta_dim(family: int, n: int, m: int) -> int:

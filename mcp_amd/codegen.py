@@ -58,7 +58,9 @@ ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
 GEN_VERSION = 2
 _MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function")
-_MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "../../include/mcpx.h")
+_MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "ipm_wg.h",
+                "ipm_wg_impl.hpp", "../../include/mcpx.h")
+WG_LDS_LIMIT = 160 * 1024 - 2048  # MCPX_NL_WG_LIMIT of csrc/ipm_nl_kernel.hpp
 LDS_LIMIT = 160 * 1024 - 2048  # bytes of static LDS one workgroup may declare on gfx950 (minus headroom)
 
 _FUNCS = {  # sympy function → C name (both libm and HIP device math)
@@ -214,15 +216,26 @@ class NLSystem:
             "dense": 1 <= n + 2 * m <= 64,
         }
 
+    def wg_solvers(self) -> dict:
+        """Workgroup-per-instance kernels of the module (MCPX_NL_CAN_WG_* of
+        csrc/ipm_nl_kernel.hpp): LDS = 3·8·(n+2m) + NS·(16·8 + 7) + 512 bytes."""
+        n, m = self.n, self.m
+        lds = lambda ns: 8 * 3 * (n + 2 * m) + ns * (8 * 16 + 7) + 512
+        return {
+            "schur": (not self.has_s) and n >= 1 and lds(n) <= WG_LDS_LIMIT,
+            "reduced": n + m >= 1 and lds(n + m) <= WG_LDS_LIMIT,
+            "dense": n + 2 * m >= 1 and lds(n + 2 * m) <= WG_LDS_LIMIT,
+        }
+
     def default_solver(self) -> str:
-        ok = self.solvers()
-        for s in ("schur", "reduced", "dense"):
-            if ok[s]:
-                return s
-        raise NotImplementedError(
-            f"nonlinear MCP with n={self.n}, m={self.m} exceeds the one-wave kernels (schur: dH/dy = 0, "
-            f"n <= 64, m <= 128; reduced: n + m <= 64; dense: n + 2m <= 64) — the workgroup-per-instance "
-            f"blocked LU is SURVEY.md §8(f) #2's remaining half")
+        """The cheapest elimination a kernel exists for: SCHUR, then REDUCED, then
+        DENSE; the one-wave kernels when the system fits them, else the
+        workgroup-per-instance ones (the C ABI picks the kernel the same way)."""
+        for ok in (self.solvers(), self.wg_solvers()):
+            for s in ("schur", "reduced", "dense"):
+                if ok[s]:
+                    return s
+        raise NotImplementedError(f"nonlinear MCP with n={self.n}, m={self.m} exceeds every kernel's LDS budget")
 
     # ---- emission ------------------------------------------------------------
     def _block(self, entries, with_z: bool) -> list:

@@ -348,13 +348,59 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   (!MCPX_NL_HAS_S && MCPX_NL_N >= 1 && MCPX_NL_N <= 64 && MCPX_NL_M <= 128 &&                         \
    MCPX_NL_SCHUR_LDS <= 160 * 1024 - 2048)
 
-// mcpx_nl_meta: {layout version, n, m, p, has_s, kernel mask (bit MCPX_LINSOLVE_*), block size, nnz}
+// ---- workgroup-per-instance kernels (ipm_wg_impl.hpp) for systems beyond one wave --
+// LDS of solve_instances<…, NV = n + 2m, NS>: z, F, δz (3·NV doubles) and the LU
+// panel + row lists (NS·(16·8 + 7) bytes), plus reduction scratch.
+#define MCPX_NL_NV (MCPX_NL_N + 2 * MCPX_NL_M)
+#define MCPX_NL_WG_LDS(NS) (8 * 3 * MCPX_NL_NV + (NS) * (8 * 16 + 7) + 512)
+#define MCPX_NL_WG_LIMIT (160 * 1024 - 2048)
+#define MCPX_NL_CAN_WG_REDUCED (MCPX_NL_N + MCPX_NL_M >= 1 && MCPX_NL_WG_LDS(MCPX_NL_N + MCPX_NL_M) <= MCPX_NL_WG_LIMIT)
+#define MCPX_NL_CAN_WG_DENSE (MCPX_NL_NV >= 1 && MCPX_NL_WG_LDS(MCPX_NL_NV) <= MCPX_NL_WG_LIMIT)
+#define MCPX_NL_CAN_WG_SCHUR (!MCPX_NL_HAS_S && MCPX_NL_N >= 1 && MCPX_NL_WG_LDS(MCPX_NL_N) <= MCPX_NL_WG_LIMIT)
+
+#include "ipm_wg_impl.hpp"
+
+namespace mcpx {
+namespace nl {
+// the generated code, as the workgroup solver's GEN policy
+struct Gen {
+  static constexpr int OFF_P = nl::OFF_P, OFF_Q = nl::OFF_Q, OFF_R = nl::OFF_R, OFF_G = nl::OFF_G,
+                       OFF_H = nl::OFF_H, OFF_S = nl::OFF_S, SIZE = MCPX_NL_SIZE;
+  static constexpr bool HAS_S = nl::HAS_S;
+  __device__ static void init(const double* th, double* blk) { mcpx_nl_init(th, blk); }
+  __device__ static void eval(const double* th, const double* z, double* blk) { mcpx_nl_eval(th, z, blk); }
+};
+constexpr int NVW = imax(1, N);
+}  // namespace nl
+}  // namespace mcpx
+
+// mcpx_nl_meta: {layout version, n, m, p, has_s, kernel mask, block size, nnz}; kernel
+// mask: bit MCPX_LINSOLVE_* = one-wave kernel, bit 3 + MCPX_LINSOLVE_* = workgroup kernel
 extern "C" {
 __device__ int32_t mcpx_nl_meta[8] = {
-    1, MCPX_NL_N, MCPX_NL_M, MCPX_NL_P, MCPX_NL_HAS_S,
+    2, MCPX_NL_N, MCPX_NL_M, MCPX_NL_P, MCPX_NL_HAS_S,
     (MCPX_NL_CAN_REDUCED << MCPX_LINSOLVE_REDUCED) | (MCPX_NL_CAN_DENSE << MCPX_LINSOLVE_DENSE) |
-        (MCPX_NL_CAN_SCHUR << MCPX_LINSOLVE_SCHUR),
+        (MCPX_NL_CAN_SCHUR << MCPX_LINSOLVE_SCHUR) | (MCPX_NL_CAN_WG_REDUCED << (3 + MCPX_LINSOLVE_REDUCED)) |
+        (MCPX_NL_CAN_WG_DENSE << (3 + MCPX_LINSOLVE_DENSE)) | (MCPX_NL_CAN_WG_SCHUR << (3 + MCPX_LINSOLVE_SCHUR)),
     MCPX_NL_SIZE, MCPX_NL_NNZ};
+
+#if MCPX_NL_CAN_WG_REDUCED
+__global__ __launch_bounds__(256) void mcpx_nl_solve_reduced_wg(const mcpx::wg::WgArgs args) {
+  mcpx::wg::solve_instances<MCPX_FAMILY_NONLINEAR, MCPX_LINSOLVE_REDUCED, mcpx::nl::NVW, MCPX_NL_N + MCPX_NL_M,
+                            mcpx::nl::Gen>(args);
+}
+#endif
+#if MCPX_NL_CAN_WG_DENSE
+__global__ __launch_bounds__(256) void mcpx_nl_solve_dense_wg(const mcpx::wg::WgArgs args) {
+  mcpx::wg::solve_instances<MCPX_FAMILY_NONLINEAR, MCPX_LINSOLVE_DENSE, mcpx::nl::NVW, mcpx::nl::NVW,
+                            mcpx::nl::Gen>(args);
+}
+#endif
+#if MCPX_NL_CAN_WG_SCHUR
+__global__ __launch_bounds__(256) void mcpx_nl_solve_schur_wg(const mcpx::wg::WgArgs args) {
+  mcpx::wg::solve_instances<MCPX_FAMILY_NONLINEAR, MCPX_LINSOLVE_SCHUR, mcpx::nl::NVW, MCPX_NL_N, mcpx::nl::Gen>(args);
+}
+#endif
 
 #if MCPX_NL_CAN_REDUCED
 __global__ __launch_bounds__(64) void mcpx_nl_solve_reduced(const mcpx::KernelArgs args) {

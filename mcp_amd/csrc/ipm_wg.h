@@ -1,0 +1,40 @@
+// ipm_wg.h — launch record and launchers of the workgroup-per-instance solver
+// (ipm_wg_impl.hpp) for KKT systems beyond the one-wave kernels' 64 rows.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ipm_kernel.h"
+
+namespace mcpx {
+namespace wg {
+
+// The one-wave kernels' KernelArgs plus the work queue and the per-slot workspace
+// (mcpx_api.cpp sizes it; one slot per resident workgroup).
+struct WgArgs {
+  KernelArgs k;
+  double* work;         // grid slots × slot_stride doubles
+  int32_t* counter;     // work-queue head, zeroed before the launch
+  int64_t batch;        // instances
+  int64_t slot_stride;  // doubles per slot
+  int64_t off_blk;      // nonlinear family: generated Jacobian blocks (MCPX_NL_SIZE doubles)
+  int64_t off_rd;       // SCHUR: R·D⁻¹ (m × n, row k = constraint k)
+  int64_t off_aux;      // SCHUR: D⁻¹, 1/w, ry, ty (4 × m)
+  int32_t ld;           // row stride of [K | rhs] (≥ ns + 1)
+  int32_t pad_;
+};
+
+constexpr int kThreads = 256;       // workgroup size of every workgroup kernel
+constexpr int kMaxDim = 768;        // largest system / vector dimension of the QP / affine kernels
+constexpr int kDimBuckets[4] = {128, 256, 512, 768};
+
+}  // namespace wg
+
+// QP / affine families, MCPX_LINSOLVE_REDUCED or _DENSE, vector dimension
+// n + 2m ≤ nv ∈ wg::kDimBuckets.  The kernel symbol (for the occupancy query)
+// and the launch; hipErrorInvalidValue when no such kernel exists.
+const void* ipm_wg_kernel(int family, int solver, int nv);
+hipError_t launch_ipm_wg(int family, int solver, int nv, const wg::WgArgs& a, int grid, hipStream_t st);
+
+}  // namespace mcpx

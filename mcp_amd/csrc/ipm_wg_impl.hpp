@@ -1,0 +1,627 @@
+// ipm_wg_impl.hpp — workgroup-per-instance solver for KKT systems too large for
+// one wave (the register-resident kernels of ipm_kernel_impl.hpp stop at 64
+// rows).  SURVEY.md §8(f) #2: the reference's trajectory games reach KKT
+// dimension 700 at horizon T = 10 (benchmark/trajectory_game_benchmark.jl:38).
+//
+// One workgroup of 256 threads (4 waves) runs the whole ϵ-continuation / Newton
+// loop of src/solver.jl:64-121 for one instance at a time, taking instances from
+// an atomic work queue (grid = the resident workgroups, so imbalance between
+// instances — 12 to 931 Newton steps — evens out).  Per workgroup slot the host
+// allocates a workspace in HBM: the linear system [K | rhs] row-major (ld ≥ NS+1)
+// and, for the nonlinear family, the generated Jacobian blocks.
+//
+// The Newton system is factored by a right-looking blocked LU with partial
+// pivoting that reproduces oracle/ipm_oracle.c::lu_solve bit for bit:
+//   * implicit pivoting: rows are never moved; the remaining rows are kept as a
+//     list in ascending row order, and the pivot of column k is the first
+//     remaining row of largest |a_ik| (NaN never wins; all-NaN → first row);
+//   * panel of NB = 16 columns staged in LDS and factored column by column
+//     (multipliers l_i = a_ik / pivot, a_ij ← fma(−l_i, u_j, a_ij));
+//   * the panel's pivot rows get their trailing part (U12, the rhs included) by
+//     the in-panel forward substitution — the same fma chain the unblocked
+//     elimination applies to them;
+//   * every other remaining row gets the trailing update C ← C + (−L21)·U12 on
+//     the matrix cores: v_mfma_f64_16x16x4_f64 equals an ordered k-ascending fma
+//     chain bitwise (tools/ubench_mfma64.hip), so each entry sees
+//     exactly the oracle's sequence fma(−l_ik, u_kj, ·), k ascending; a panel
+//     width that is not a multiple of 4 finishes on the VALU in the same order;
+//   * column-oriented back substitution, x_k = b_p / u_pk.
+// Residual, Jacobian rows, slack / y eliminations, line search and update follow
+// the oracle's solve_one() op for op (same fma chains, same order).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ipm_wg.h"
+
+namespace mcpx {
+namespace wg {
+
+constexpr int WG = 256;  // threads per workgroup
+constexpr int NWAVE = WG / 64;
+constexpr int NB = 16;   // LU panel width
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ---- workgroup reductions (all threads call; result uniform) ----------------
+
+struct Scratch {
+  double d[NWAVE];
+  uint64_t u[NWAVE];
+  uint64_t u2[NWAVE];
+  int32_t i[NWAVE];
+  int32_t inst;
+};
+
+__device__ __forceinline__ double max_nan(double a, double b) { return (a != a || b != b) ? a + b : fmax(a, b); }
+
+__device__ __forceinline__ double shfl_xor_d(double v, int m) {
+  const int lo = __shfl_xor(__double2loint(v), m), hi = __shfl_xor(__double2hiint(v), m);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// NaN-propagating max of non-negative values (‖F‖∞ of src/solver.jl:107).
+__device__ __forceinline__ double wg_max_nan(double v, Scratch& s) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max_nan(v, shfl_xor_d(v, o));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s.d[w] = v;
+  __syncthreads();
+  double r = s.d[0];
+#pragma unroll
+  for (int q = 1; q < NWAVE; ++q) r = max_nan(r, s.d[q]);
+  return r;
+}
+
+__device__ __forceinline__ uint64_t wg_or(uint64_t v, Scratch& s) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v |= shfl_xor_u64(v, o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) s.u[w] = v;
+  __syncthreads();
+  uint64_t r = 0;
+#pragma unroll
+  for (int q = 0; q < NWAVE; ++q) r |= s.u[q];
+  return r;
+}
+
+// Largest key, ties to the smallest position (pos < 0: no candidate).
+__device__ __forceinline__ void better(uint64_t& k, int& p, uint64_t k2, int p2) {
+  if (k2 > k || (k2 == k && p2 >= 0 && (p < 0 || p2 < p))) {
+    k = k2;
+    p = p2;
+  }
+}
+__device__ __forceinline__ int wg_argmax(uint64_t key, int pos, Scratch& s) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t k2 = shfl_xor_u64(key, o);
+    const int p2 = __shfl_xor(pos, o);
+    better(key, pos, k2, p2);
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    s.u2[w] = key;
+    s.i[w] = pos;
+  }
+  __syncthreads();
+  uint64_t k = s.u2[0];
+  int p = s.i[0];
+#pragma unroll
+  for (int q = 1; q < NWAVE; ++q) better(k, p, s.u2[q], s.i[q]);
+  return p;
+}
+
+// Pivot-search key of a remaining row: NaN never wins over a number (oracle:
+// `v > bv` is false for NaN), an all-NaN column takes the first remaining row.
+__device__ __forceinline__ uint64_t pivot_key(double a) {
+  const double v = fabs(a);
+  if (v != v) return 1ull;
+  return (uint64_t)__double_as_longlong(v) + 2ull;
+}
+
+// ---- blocked LU with partial pivoting (oracle lu_solve) --------------------
+//
+// A: ns × (ns + 1) row-major with stride ld, column ns = rhs; destroyed.
+// LDS: pan[NSMAX·NB], rem/ispiv/step/prow[NSMAX], x[NSMAX] (solution out).
+template <int NSMAX>
+struct LuShared {
+  double pan[NSMAX * NB];
+  int16_t rem[NSMAX];
+  int16_t step_of[NSMAX];
+  int16_t prow[NSMAX];
+  int16_t pivpos[NB];
+  uint8_t ispiv[NSMAX];
+  int32_t cnt[NWAVE];
+};
+
+template <int NSMAX>
+__device__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuShared<NSMAX>& L, Scratch& sc) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < ns; i += WG) L.rem[i] = (int16_t)i;
+  int r = ns;  // remaining rows (list length)
+  __syncthreads();
+  for (int k0 = 0; k0 < ns; k0 += NB) {
+    const int kb = min(NB, ns - k0);
+    // ---- stage the panel columns [k0, k0+kb) of the remaining rows ---------
+    for (int idx = tid; idx < r * NB; idx += WG) {
+      const int pos = idx / NB, kk = idx - pos * NB;
+      if (kk < kb) L.pan[idx] = A[(int64_t)L.rem[pos] * ld + k0 + kk];
+    }
+    for (int pos = tid; pos < r; pos += WG) L.ispiv[pos] = 0;
+    __syncthreads();
+    // ---- factor the panel column by column ----------------------------------
+    for (int kk = 0; kk < kb; ++kk) {
+      uint64_t key = 0;
+      int pos = -1;
+      for (int q = tid; q < r; q += WG)
+        if (!L.ispiv[q]) better(key, pos, pivot_key(L.pan[q * NB + kk]), q);
+      const int pp = wg_argmax(key, pos, sc);
+      const double piv = L.pan[pp * NB + kk];
+      if (piv == 0.0) return false;  // the failed linear solve of src/solver.jl:84-88
+      if (tid == 0) {
+        L.ispiv[pp] = 1;
+        L.pivpos[kk] = (int16_t)pp;
+        L.prow[k0 + kk] = L.rem[pp];
+        L.step_of[L.rem[pp]] = (int16_t)(k0 + kk);
+      }
+      __syncthreads();
+      for (int q = tid; q < r; q += WG) {
+        if (L.ispiv[q]) continue;
+        double* row = L.pan + q * NB;
+        const double l = row[kk] / piv;
+        for (int jj = kk + 1; jj < kb; ++jj) row[jj] = fma(-l, L.pan[pp * NB + jj], row[jj]);
+        row[kk] = l;  // a_ik of a remaining row is never read again: keep l_ik there
+      }
+      __syncthreads();
+    }
+    // panel back to A: U11 in the pivot rows (their left part holds multipliers, never read)
+    for (int idx = tid; idx < r * NB; idx += WG) {
+      const int pos = idx / NB, kk = idx - pos * NB;
+      if (kk < kb) A[(int64_t)L.rem[pos] * ld + k0 + kk] = L.pan[idx];
+    }
+    // ---- U12: in-panel forward substitution of the pivot rows' trailing part -
+    const int j_lo = k0 + kb;  // trailing columns j_lo .. ns (rhs = column ns)
+    for (int j = j_lo + tid; j <= ns; j += WG) {
+      double u[NB];
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk) {
+        if (kk >= kb) continue;
+        const int pp = L.pivpos[kk];
+        double v = A[(int64_t)L.rem[pp] * ld + j];
+#pragma unroll
+        for (int k2 = 0; k2 < NB; ++k2)
+          if (k2 < kk) v = fma(-L.pan[pp * NB + k2], u[k2], v);
+        u[kk] = v;
+        A[(int64_t)L.rem[pp] * ld + j] = v;
+      }
+    }
+    __syncthreads();
+    // ---- trailing update of the other remaining rows on the matrix cores -----
+    const int ncol = ns + 1 - j_lo;
+    if (ncol > 0 && r > kb) {
+      const int rt = (r + 15) / 16, ct = (ncol + 15) / 16;
+      const int kfull = kb & ~3;
+      const int lr = lane >> 4, lc = lane & 15;
+      for (int t = wave; t < rt * ct; t += NWAVE) {
+        const int ti = t / ct, tj = t - ti * ct;
+        const int j = j_lo + 16 * tj + lc;
+        const bool jin = j <= ns;
+        d4 acc;
+        int rowp[4];
+        bool rin[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int pos = 16 * ti + lr + 4 * e;
+          rin[e] = pos < r && !L.ispiv[pos < r ? pos : 0];
+          rowp[e] = pos < r ? L.rem[pos] : 0;
+          acc[e] = (rin[e] && jin) ? A[(int64_t)rowp[e] * ld + j] : 0.0;
+        }
+        const int pa = 16 * ti + lc;  // A-fragment row of this lane
+        for (int c = 0; c < kfull; c += 4) {
+          const int kk = c + lr;
+          const double a = pa < r ? -L.pan[pa * NB + kk] : 0.0;
+          const double b = jin ? A[(int64_t)L.rem[L.pivpos[kk]] * ld + j] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        }
+        for (int kk = kfull; kk < kb; ++kk) {  // panel width not a multiple of 4: same order on the VALU
+          const double b = jin ? A[(int64_t)L.rem[L.pivpos[kk]] * ld + j] : 0.0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int pos = 16 * ti + lr + 4 * e;
+            const double l = pos < r ? L.pan[pos * NB + kk] : 0.0;
+            acc[e] = fma(-l, b, acc[e]);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (rin[e] && jin) A[(int64_t)rowp[e] * ld + j] = acc[e];
+      }
+    }
+    __syncthreads();
+    // ---- drop the panel's pivot rows from the remaining list (stable) --------
+    // A kept row only moves left (dst ≤ pos), and every source of a chunk is read
+    // before the barrier that precedes its writes, so the list compacts in place.
+    int base = 0;
+    for (int c0 = 0; c0 < r; c0 += WG) {
+      const int pos = c0 + tid;
+      const bool f = pos < r && !L.ispiv[pos < r ? pos : 0];
+      const int16_t v = pos < r ? L.rem[pos] : (int16_t)0;
+      const uint64_t bal = __ballot(f);
+      const int before = __popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) L.cnt[wave] = __popcll(bal);
+      __syncthreads();
+      int off = base, tot = 0;
+#pragma unroll
+      for (int q = 0; q < NWAVE; ++q) {
+        off += (q < wave) ? L.cnt[q] : 0;
+        tot += L.cnt[q];
+      }
+      __syncthreads();  // every thread has read cnt and its source entry
+      if (f) L.rem[off + before] = v;
+      base += tot;
+    }
+    r = base;
+    __syncthreads();
+  }
+  // ---- back substitution (column-oriented, oracle order) ----------------------
+  constexpr int RPT = (NSMAX + WG - 1) / WG;  // rows per thread
+  double b[RPT];
+  int st[RPT];
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int i = q * WG + tid;
+    b[q] = i < ns ? A[(int64_t)i * ld + ns] : 0.0;
+    st[q] = i < ns ? L.step_of[i] : 0x7fff;
+  }
+  for (int k = ns - 1; k >= 0; --k) {
+    const int p = L.prow[k];
+    if ((p & (WG - 1)) == tid) {
+      double bp = 0.0;
+#pragma unroll
+      for (int q = 0; q < RPT; ++q)
+        if (q == p / WG) bp = b[q];
+      x[k] = bp / A[(int64_t)p * ld + k];
+    }
+    __syncthreads();
+    const double xk = x[k];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int i = q * WG + tid;
+      if (i < ns && st[q] < k) b[q] = fma(-A[(int64_t)i * ld + k], xk, b[q]);
+    }
+  }
+  __syncthreads();
+  return true;
+}
+
+// ---- the solver -------------------------------------------------------------
+
+// The generated code of a nonlinear module (csrc/ipm_nl_kernel.hpp) or nothing.
+struct NoGen {
+  static constexpr int OFF_P = 0, OFF_Q = 0, OFF_R = 0, OFF_G = 0, OFF_H = 0, OFF_S = 0, SIZE = 0;
+  static constexpr bool HAS_S = false;
+  __device__ static void init(const double*, double*) {}
+  __device__ static void eval(const double*, const double*, double*) {}
+};
+
+// Row i of F (src/mcp.jl:76-80) at z = zs, oracle family_row() op for op.
+template <int FAMILY, class GEN>
+__device__ __forceinline__ double residual(const double* __restrict__ th, const double* __restrict__ blk,
+                                           const double* zs, int n, int m, double eps, int i) {
+  const int nn = n * n, nm = n * m, mm = m * m;
+  if (i < n) {
+    if constexpr (FAMILY == MCPX_FAMILY_NONLINEAR) {
+      return blk[GEN::OFF_G + i];
+    } else {
+      double acc = 0.0;
+      for (int j = 0; j < n; ++j) acc = fma(th[j * n + i], zs[j], acc);  // M_ij / P_ij
+      if constexpr (FAMILY == MCPX_FAMILY_QP) {
+        for (int k = 0; k < m; ++k) acc = fma(-th[nn + i * m + k], zs[n + k], acc);  // −A_ki
+        return acc - th[nn + nm + m + i];                                           // − ϕ_i
+      } else {
+        for (int k = 0; k < m; ++k) acc = fma(th[nn + k * n + i], zs[n + k], acc);   // Q_ik
+        return acc + th[nn + 2 * nm + mm + i];                                      // + g_i
+      }
+    }
+  } else if (i < n + m) {
+    const int k = i - n;
+    if constexpr (FAMILY == MCPX_FAMILY_NONLINEAR) {
+      return blk[GEN::OFF_H + k] - zs[n + m + k];
+    } else {
+      double acc = 0.0;
+      if constexpr (FAMILY == MCPX_FAMILY_QP) {
+        for (int j = 0; j < n; ++j) acc = fma(th[nn + j * m + k], zs[j], acc);  // A_kj
+        return (acc - th[nn + nm + k]) - zs[n + m + k];
+      } else {
+        for (int j = 0; j < n; ++j) acc = fma(th[nn + nm + j * m + k], zs[j], acc);  // R_kj
+        for (int q = 0; q < m; ++q) acc = fma(th[nn + 2 * nm + q * m + k], zs[n + q], acc);  // S_kq
+        return (acc + th[nn + 2 * nm + mm + n + k]) - zs[n + m + k];
+      }
+    }
+  }
+  const int k = i - n - m;
+  return zs[n + m + k] * zs[n + k] - eps;  // s ⊙ y − ϵ
+}
+
+// ∇F_z[i][j] without tol·I (src/mcp.jl:97-120), oracle family_row() entries.
+template <int FAMILY, class GEN>
+__device__ __forceinline__ double jac(const double* __restrict__ th, const double* __restrict__ blk,
+                                      const double* zs, int n, int m, int i, int j) {
+  const int nn = n * n, nm = n * m;
+  if (i < n) {  // G rows
+    if (j < n) return FAMILY == MCPX_FAMILY_NONLINEAR ? blk[GEN::OFF_P + j * n + i] : th[j * n + i];
+    if (j < n + m) {
+      const int k = j - n;
+      if constexpr (FAMILY == MCPX_FAMILY_QP) return -th[nn + i * m + k];
+      else if constexpr (FAMILY == MCPX_FAMILY_NONLINEAR) return blk[GEN::OFF_Q + k * n + i];
+      else return th[nn + k * n + i];
+    }
+    return 0.0;
+  }
+  if (i < n + m) {  // H − s rows
+    const int k = i - n;
+    if (j < n) {
+      if constexpr (FAMILY == MCPX_FAMILY_QP) return th[nn + j * m + k];
+      else if constexpr (FAMILY == MCPX_FAMILY_NONLINEAR) return blk[GEN::OFF_R + j * m + k];
+      else return th[nn + nm + j * m + k];
+    }
+    if (j < n + m) {
+      const int q = j - n;
+      if constexpr (FAMILY == MCPX_FAMILY_QP) return 0.0;
+      else if constexpr (FAMILY == MCPX_FAMILY_NONLINEAR) return GEN::HAS_S ? blk[GEN::OFF_S + q * m + k] : 0.0;
+      else return th[nn + 2 * nm + q * m + k];
+    }
+    return (j - n - m == k) ? -1.0 : 0.0;
+  }
+  const int k = i - n - m;  // s ⊙ y − ϵ rows
+  if (j == n + k) return zs[n + m + k];
+  if (j == n + m + k) return zs[n + k];
+  return 0.0;
+}
+
+template <int NVMAX, int NSMAX>
+struct SolveShared {
+  double zs[NVMAX], Fs[NVMAX], dzs[NVMAX];
+  LuShared<NSMAX> lu;
+  Scratch sc;
+};
+
+template <int FAMILY, int SOLVER, int NVMAX, int NSMAX, class GEN>
+__device__ void solve_instances(const WgArgs& W) {
+  constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR, RED = SOLVER == MCPX_LINSOLVE_REDUCED;
+  constexpr bool NL = FAMILY == MCPX_FAMILY_NONLINEAR;
+  static_assert(!SCH || (NL && !GEN::HAS_S), "the workgroup SCHUR path is the nonlinear family's (dH/dy = 0)");
+  __shared__ SolveShared<NVMAX, NSMAX> S;
+  const KernelArgs& a = W.k;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int n = a.n, m = a.m, N = n + 2 * m;
+  const int ns = SCH ? n : (RED ? n + m : N);
+  const int ld = W.ld;
+  const double tol = a.tol;
+  double* const slot = W.work + (int64_t)blockIdx.x * W.slot_stride;
+  double* const Am = slot;
+  double* const blk = slot + W.off_blk;
+  double* const RD = slot + W.off_rd;
+  double* const sD = slot + W.off_aux;
+  double* const srw = sD + m;
+  double* const sry = sD + 2 * m;
+  double* const sty = sD + 3 * m;
+  double* const zs = S.zs;
+  double* const Fs = S.Fs;
+  double* const dzs = S.dzs;
+
+  for (;;) {
+    if (tid == 0) S.sc.inst = atomicAdd(W.counter, 1);  // the work queue
+    __syncthreads();
+    const int64_t inst = S.sc.inst;
+    __syncthreads();
+    if (inst >= W.batch) break;  // every workgroup reaches this exit
+    const double* __restrict__ th = a.theta + inst * a.theta_ld;
+
+    // src/solver.jl:39-41, 64-66: x₀ = 0, y₀ = 1, s₀ = 1 unless warm-started
+    for (int i = tid; i < N; i += WG) {
+      double v;
+      if (i < n) v = a.x0 ? a.x0[inst * n + i] : 0.0;
+      else if (i < n + m) v = a.y0 ? a.y0[inst * m + (i - n)] : 1.0;
+      else v = a.s0 ? a.s0[inst * m + (i - n - m)] : 1.0;
+      zs[i] = v;
+    }
+    if constexpr (NL) {
+      for (int i = tid; i < GEN::SIZE; i += WG) blk[i] = 0.0;  // structural zeros
+      __syncthreads();
+      if (tid == 0) GEN::init(th, blk);
+    }
+    __syncthreads();
+
+    double eps = 1.0;                   // :67
+    double kkt = __builtin_huge_val();  // :68
+    int status = 0;                     // :69
+    int outer = 1;                      // :70
+    int newton = 0;
+    while (kkt > tol && eps > tol && outer < a.max_outer) {  // :71
+      int inner = 1;                                          // :72
+      status = 0;                                             // :73
+      while (kkt > eps && inner < a.max_inner) {              // :75
+        // ---- F!, ∇F_z! (:79-81) ------------------------------------------------
+        if constexpr (NL) {
+          if (tid == 0) GEN::eval(th, zs, blk);
+          __syncthreads();
+        }
+        double mx = 0.0;
+        for (int i = tid; i < N; i += WG) {
+          const double f = residual<FAMILY, GEN>(th, blk, zs, n, m, eps, i);
+          Fs[i] = f;
+          mx = max_nan(mx, fabs(f));
+        }
+        const double kkt_step = wg_max_nan(mx, S.sc);  // ‖F‖∞ (:107), committed after the step
+        // ---- the Newton system (:81-83) as [K | rhs] -------------------------------
+        if constexpr (SCH) {
+          // eliminate δs_k (pivot w_k = y_k + tol), then δy_k (pivot D_k = (0 + tol) + s_k / w_k)
+          for (int k = tid; k < m; k += WG) {
+            const double rw = 1.0 / (zs[n + k] + tol);
+            const double D = (0.0 + tol) + zs[n + m + k] * rw;
+            const double Di = 1.0 / D;
+            const double ry = (-Fs[n + k]) - (Fs[n + m + k] * rw);
+            sD[k] = Di;
+            srw[k] = rw;
+            sry[k] = ry;
+            sty[k] = ry * Di;
+          }
+          __syncthreads();
+          for (int idx = tid; idx < m * n; idx += WG) {  // R_kj · D_k⁻¹, row k
+            const int k = idx / n, j = idx - k * n;
+            RD[idx] = blk[GEN::OFF_R + j * m + k] * sD[k];
+          }
+          __syncthreads();
+          // S = (P + tol·I) + Σ_k (−Q_ik)(R_kj D_k⁻¹), k ascending, on the matrix cores
+          const int nt = (n + 15) / 16, wave = tid >> 6, lr = lane >> 4, lc = lane & 15;
+          const int mfull = m & ~3;
+          for (int t = wave; t < nt * nt; t += NWAVE) {
+            const int ti = t / nt, tj = t - ti * nt;
+            const int j = 16 * tj + lc;
+            d4 acc;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int i = 16 * ti + lr + 4 * e;
+              const double p = (i < n && j < n) ? blk[GEN::OFF_P + j * n + i] : 0.0;
+              acc[e] = (i == j) ? p + tol : p;
+            }
+            const int ia = 16 * ti + lc;
+            for (int c = 0; c < mfull; c += 4) {
+              const int k = c + lr;
+              const double av = ia < n ? -blk[GEN::OFF_Q + k * n + ia] : 0.0;
+              const double bv = j < n ? RD[k * n + j] : 0.0;
+              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+            for (int k = mfull; k < m; ++k) {  // m not a multiple of 4: the rest on the VALU, same order
+              const double bv = j < n ? RD[k * n + j] : 0.0;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int i = 16 * ti + lr + 4 * e;
+                acc[e] = fma(i < n ? -blk[GEN::OFF_Q + k * n + i] : 0.0, bv, acc[e]);
+              }
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int i = 16 * ti + lr + 4 * e;
+              if (i < n && j < n) Am[(int64_t)i * ld + j] = acc[e];
+            }
+          }
+          for (int i = tid; i < n; i += WG) {  // rr_i = −F_Gi + Σ_k (−Q_ik) ty_k
+            double acc = -Fs[i];
+            for (int k = 0; k < m; ++k) acc = fma(-blk[GEN::OFF_Q + k * n + i], sty[k], acc);
+            Am[(int64_t)i * ld + n] = acc;
+          }
+        } else {
+          const int w1 = ns + 1;
+          for (int idx = tid; idx < ns * w1; idx += WG) {
+            const int i = idx / w1, j = idx - i * w1;
+            double v;
+            if (j < ns) {
+              v = jac<FAMILY, GEN>(th, blk, zs, n, m, i, j);
+              if (i == j) {
+                v += tol;  // src/solver.jl:81 ∇F + tol*I
+                if (RED && i >= n) v += zs[n + m + (i - n)] / (zs[i] + tol);  // + s_k / w_k
+              }
+            } else {
+              v = -Fs[i];
+              if (RED && i >= n) v = v - (Fs[i + m] / (zs[i] + tol));  // −F_H − F_C / w_k
+            }
+            Am[(int64_t)i * ld + j] = v;
+          }
+        }
+        __syncthreads();
+        // ---- LU with partial pivoting (:83-88) ------------------------------------
+        if (!lu_solve<NSMAX>(Am, ld, ns, dzs, S.lu, S.sc)) {
+          status = 1;
+          break;
+        }
+        if constexpr (SCH) {  // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
+          for (int k = tid; k < m; k += WG) {
+            double acc = sry[k];
+            for (int j = 0; j < n; ++j) acc = fma(-blk[GEN::OFF_R + j * m + k], dzs[j], acc);
+            const double dy = acc * sD[k];
+            dzs[n + k] = dy;
+            dzs[n + m + k] = fma(-zs[n + m + k], dy, -Fs[n + m + k]) * srw[k];
+          }
+        } else if constexpr (RED) {  // δs_k = (−F_Ck − s_k δy_k) / w_k
+          for (int k = tid; k < m; k += WG)
+            dzs[n + m + k] = fma(-zs[n + m + k], dzs[n + k], -Fs[n + m + k]) / (zs[n + k] + tol);
+        }
+        __syncthreads();
+        // ---- fraction-to-the-boundary line search (:93-100, :127-138) ---------------
+        uint64_t vs = 0ull, vy = 0ull;
+        for (int k = tid; k < m; k += WG) {
+          const double s = zs[n + m + k], ds = dzs[n + m + k], y = zs[n + k], dy = dzs[n + k];
+          const double cs = a.c_tau * s, cy = a.c_tau * y;
+          double alpha = 1.0;
+          for (int e = 0; e < a.n_trials; ++e) {
+            if (s + alpha * ds < cs) vs |= 1ull << e;
+            if (y + alpha * dy < cy) vy |= 1ull << e;
+            alpha *= a.decay;
+          }
+        }
+        vs = wg_or(vs, S.sc);
+        vy = wg_or(vy, S.sc);
+        const int es = (~vs) ? __ffsll((unsigned long long)~vs) - 1 : 64;
+        const int ey = (~vy) ? __ffsll((unsigned long long)~vy) - 1 : 64;
+        if (es >= a.n_trials || ey >= a.n_trials) {  // α = NaN
+          status = 1;
+          break;
+        }
+        double as = 1.0, ay = 1.0;
+        for (int e = 0; e < es; ++e) as *= a.decay;
+        for (int e = 0; e < ey; ++e) ay *= a.decay;
+        if (a.alpha_trace && newton < a.trace_len && tid == 0) {
+          uint8_t* tr = a.alpha_trace + ((size_t)inst * a.trace_len + newton) * 2;
+          tr[0] = (uint8_t)es;
+          tr[1] = (uint8_t)ey;
+        }
+        // ---- update (:103-105; x moves with α_s) ------------------------------------
+        for (int i = tid; i < N; i += WG) zs[i] = zs[i] + ((i >= n && i < n + m) ? ay : as) * dzs[i];
+        kkt = kkt_step;  // :107
+        ++inner;         // :108
+        ++newton;
+        __syncthreads();
+      }
+      eps *= (status == 0) ? a.tight[inner] : a.loose[inner];  // :111-113
+      ++outer;                                                  // :114
+    }
+    if (outer == a.max_outer) status = 1;  // :117-119
+    __syncthreads();
+
+    // ---- outputs (:121) -------------------------------------------------------------
+    for (int i = tid; i < N; i += WG) {
+      if (i < n) a.x[inst * n + i] = zs[i];
+      else if (i < n + m) a.y[inst * m + (i - n)] = zs[i];
+      else a.s[inst * m + (i - n - m)] = zs[i];
+    }
+    if (a.active_mask) {  // m ≤ 64 (checked by the host)
+      uint64_t act = 0ull;
+      for (int k = tid; k < m; k += WG)
+        if (zs[n + k] > zs[n + m + k]) act |= 1ull << k;
+      act = wg_or(act, S.sc);
+      if (tid == 0) a.active_mask[inst] = act;
+    }
+    if (tid == 0) {
+      a.kkt_error[inst] = kkt;
+      a.eps[inst] = eps;
+      a.outer_iters[inst] = outer;
+      a.status[inst] = status;
+      if (a.newton_iters) a.newton_iters[inst] = newton;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace wg
+}  // namespace mcpx

@@ -23,6 +23,7 @@
 
 #include "../../include/mcpx.h"
 #include "ipm_kernel.h"
+#include "ipm_wg.h"
 #include "sens_kernel.h"
 
 // A generated nonlinear module (MCPX_FAMILY_NONLINEAR, include/mcpx.h): the
@@ -77,9 +78,20 @@ int pick_nmax(int N) {
   return -1;
 }
 
+// Smallest workgroup-kernel vector-dimension bucket ≥ N (QP / affine), or -1.
+int pick_wg_bucket(int N) {
+  for (int w : mcpx::wg::kDimBuckets)
+    if (N <= w) return w;
+  return -1;
+}
+
 // Validates desc/params and fills the scalar part + tables of the kernel args.
+// *wg: the solve runs on the workgroup-per-instance kernels (ipm_wg_impl.hpp);
+// *nmax: the one-wave kernels' row width, or the workgroup kernels' dimension bucket.
 int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* nmax,
-            const mcpx_module* mod = nullptr) {
+            const mcpx_module* mod = nullptr, bool* wg = nullptr) {
+  bool wg_local = false;
+  if (!wg) wg = &wg_local;
   if (!d || !p) return fail(MCPX_EINVAL, "desc and params must be non-NULL");
   int64_t pd;
   if (mod) {  // a generated nonlinear module: θ dimension and sizes from its metadata
@@ -102,22 +114,34 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   const int ls = p->linear_solver;
   if (ls != MCPX_LINSOLVE_REDUCED && ls != MCPX_LINSOLVE_DENSE && ls != MCPX_LINSOLVE_SCHUR)
     return fail(MCPX_EINVAL, "unknown linear_solver %d", ls);
+  if (p->kernel != MCPX_KERNEL_AUTO && p->kernel != MCPX_KERNEL_WAVE && p->kernel != MCPX_KERNEL_WORKGROUP)
+    return fail(MCPX_EINVAL, "unknown kernel selector %d", p->kernel);
+  bool wave_ok, wg_ok;
   if (mod) {
-    if (!((mod->meta[5] >> ls) & 1))
-      return fail(MCPX_EUNSUPPORTED, "the generated module has no kernel for linear_solver=%d (n=%d m=%d; schur: "
-                  "dH/dy = 0, n <= 64, m <= 128; reduced: n+m <= 64; dense: n+2m <= 64)", ls, d->n, d->m);
+    wave_ok = (mod->meta[5] >> ls) & 1;
+    wg_ok = (mod->meta[5] >> (3 + ls)) & 1;
     *nmax = 0;
   } else {
     if (ls == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP)
       return fail(MCPX_EINVAL, "linear_solver=schur needs the QP family (dH/dy = 0)");
     const int N = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : (ls == MCPX_LINSOLVE_REDUCED ? d->n + d->m : d->n);
     const int lanes = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : d->n + d->m;  // one wave: one lane per row
-    *nmax = pick_nmax(N);
-    if (*nmax < 0 || lanes > MCPX_MAX_KKT_DIM)
-      return fail(MCPX_EUNSUPPORTED, "problem size n=%d m=%d exceeds the register-resident kernel for this "
-                  "linear_solver (reduced/schur: n+m <= %d, dense: n+2m <= %d)", d->n, d->m, MCPX_MAX_KKT_DIM,
-                  MCPX_MAX_KKT_DIM);
+    wave_ok = pick_nmax(N) > 0 && lanes <= MCPX_MAX_KKT_DIM;
+    wg_ok = ls != MCPX_LINSOLVE_SCHUR && d->n + 2 * d->m <= MCPX_MAX_WG_KKT_DIM;
+    *nmax = wave_ok && p->kernel != MCPX_KERNEL_WORKGROUP ? pick_nmax(N) : pick_wg_bucket(d->n + 2 * d->m);
   }
+  if (p->kernel == MCPX_KERNEL_WAVE) wg_ok = false;
+  if (p->kernel == MCPX_KERNEL_WORKGROUP) wave_ok = false;
+  if (!wave_ok && !wg_ok) {
+    if (mod)
+      return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel for linear_solver=%d (n=%d m=%d)",
+                  p->kernel == MCPX_KERNEL_WAVE ? "one-wave" : (p->kernel == MCPX_KERNEL_WORKGROUP ? "workgroup" : ""),
+                  ls, d->n, d->m);
+    return fail(MCPX_EUNSUPPORTED, "problem size n=%d m=%d, linear_solver=%d exceeds the kernels (one wave: "
+                "reduced/schur n+m <= %d, dense n+2m <= %d; workgroup: reduced/dense n+2m <= %d, no schur)",
+                d->n, d->m, ls, MCPX_MAX_KKT_DIM, MCPX_MAX_KKT_DIM, MCPX_MAX_WG_KKT_DIM);
+  }
+  *wg = !wave_ok;
   if (!(p->tol > 0) || !(p->min_stepsize > 0) || !(p->decay > 0 && p->decay < 1) || std::isnan(p->tau) ||
       std::isnan(p->tightening_rate) || std::isnan(p->loosening_rate) || p->max_inner_iters < 1 ||
       p->max_outer_iters < 1)
@@ -153,7 +177,7 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
 }
 
 // ---- generated nonlinear modules ---------------------------------------------
-constexpr int32_t kNLLayout = 1;  // mcpx_nl_meta[0] of csrc/ipm_nl_kernel.hpp
+constexpr int32_t kNLLayout = 2;  // mcpx_nl_meta[0] of csrc/ipm_nl_kernel.hpp
 const char* const kNLKernel[3] = {"mcpx_nl_solve_reduced", "mcpx_nl_solve_dense", "mcpx_nl_solve_schur"};
 
 // `mod` on device `dev` (the current device), loaded on first use.
@@ -169,15 +193,17 @@ int module_on(mcpx_module* mod, int dev, hipModule_t* hm) {
   return MCPX_OK;
 }
 
-// The module's kernel for linear solver `solver` on the current device.
-int nl_function(mcpx_module* mod, int solver, hipFunction_t* f) {
+// The module's kernel for linear solver `solver` (one-wave, or the workgroup
+// kernel "<name>_wg") on the current device.
+int nl_function(mcpx_module* mod, int solver, bool wg, hipFunction_t* f) {
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   hipModule_t hm;
   const int rc = module_on(mod, dev, &hm);
   if (rc) return rc;
-  if (hipModuleGetFunction(f, hm, kNLKernel[solver]) != hipSuccess)
-    return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel", kNLKernel[solver]);
+  const std::string name = std::string(kNLKernel[solver]) + (wg ? "_wg" : "");
+  if (hipModuleGetFunction(f, hm, name.c_str()) != hipSuccess)
+    return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel", name.c_str());
   return MCPX_OK;
 }
 
@@ -199,33 +225,100 @@ hipError_t launch(int nmax, const mcpx::KernelArgs& a, int64_t nb, hipStream_t s
   }
 }
 
+// Per-instance pointers of chunk [b0, b0 + nb) into the kernel args.
+void set_chunk(mcpx::KernelArgs& a, const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
+               const double* s0, const mcpx_out* o, int64_t b0) {
+  const int n = d->n, m = d->m;
+  a.theta = theta + b0 * d->theta_ld;
+  a.x0 = x0 ? x0 + b0 * n : nullptr;
+  a.y0 = y0 ? y0 + b0 * m : nullptr;
+  a.s0 = s0 ? s0 + b0 * m : nullptr;
+  a.x = o->x + b0 * n;
+  a.y = o->y + b0 * m;
+  a.s = o->s + b0 * m;
+  a.kkt_error = o->kkt_error + b0;
+  a.eps = o->eps + b0;
+  a.outer_iters = o->outer_iters + b0;
+  a.status = o->status + b0;
+  a.newton_iters = o->newton_iters ? o->newton_iters + b0 : nullptr;
+  a.active_mask = o->active_mask ? o->active_mask + b0 : nullptr;
+  a.alpha_trace = (o->alpha_trace && o->trace_len > 0) ? o->alpha_trace + b0 * (int64_t)o->trace_len * 2 : nullptr;
+  a.trace_len = o->alpha_trace ? o->trace_len : 0;
+}
+
+// Workgroup-per-instance launch (ipm_wg_impl.hpp): a persistent grid of the
+// resident workgroups pulls instances from an atomic counter; each workgroup
+// slot owns a workspace in HBM ([K | rhs] row-major, and for a generated module
+// its Jacobian blocks), allocated stream-ordered for this call.
+int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const double* y0, const double* s0,
+              const mcpx_out* o, mcpx::KernelArgs a, int nv, hipStream_t st, mcpx_module* mod) {
+  const int n = d->n, m = d->m, ls = a.solver;
+  const int ns = ls == MCPX_LINSOLVE_SCHUR ? n : (ls == MCPX_LINSOLVE_REDUCED ? n + m : n + 2 * m);
+  hipFunction_t f = nullptr;
+  const void* kp = nullptr;
+  int per_cu = 0;
+  if (mod) {
+    const int rc = nl_function(mod, ls, true, &f);
+    if (rc) return rc;
+    HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, mcpx::wg::kThreads, 0));
+  } else {
+    kp = mcpx::ipm_wg_kernel(a.family, ls, nv);
+    if (!kp) return fail(MCPX_EUNSUPPORTED, "no workgroup kernel for family %d, linear_solver %d, dim %d", a.family, ls, nv);
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, mcpx::wg::kThreads, 0));
+  }
+  int dev = 0, cus = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t slots_max = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+  auto align = [](int64_t v) { return (v + 31) / 32 * 32; };  // 256-B boundaries
+  mcpx::wg::WgArgs w{};
+  w.ld = ns + 1;
+  w.off_blk = align((int64_t)ns * w.ld);
+  w.off_rd = align(w.off_blk + (mod ? mod->meta[6] : 0));
+  w.off_aux = align(w.off_rd + (ls == MCPX_LINSOLVE_SCHUR ? (int64_t)m * n : 0));
+  w.slot_stride = align(w.off_aux + (ls == MCPX_LINSOLVE_SCHUR ? 4 * (int64_t)m : 0));
+  const int64_t CH = (int64_t)1 << 30;
+  const int64_t grid_max = std::min(slots_max, std::min(CH, d->batch));
+  double* ws = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)(grid_max * w.slot_stride) + 256;
+  HIP_TRY(hipMallocAsync((void**)&ws, bytes, st));
+  w.work = ws;
+  w.counter = (int32_t*)(ws + grid_max * w.slot_stride);
+  int rc = MCPX_OK;
+  for (int64_t b0 = 0; b0 < d->batch && rc == MCPX_OK; b0 += CH) {
+    const int64_t nb = std::min(CH, d->batch - b0);
+    const int grid = (int)std::min(grid_max, nb);
+    set_chunk(a, d, theta, x0, y0, s0, o, b0);
+    w.k = a;
+    w.batch = nb;
+    hipError_t e = hipMemsetAsync(w.counter, 0, sizeof(int32_t), st);
+    if (e == hipSuccess) {
+      if (mod) {
+        void* params[] = {&w};
+        e = hipModuleLaunchKernel(f, (unsigned)grid, 1, 1, mcpx::wg::kThreads, 1, 1, 0, st, params, nullptr);
+      } else {
+        e = mcpx::launch_ipm_wg(a.family, ls, nv, w, grid, st);
+      }
+    }
+    if (e != hipSuccess) rc = fail(MCPX_EHIP, "workgroup solver launch failed: %s", hipGetErrorString(e));
+  }
+  HIP_TRY(hipFreeAsync(ws, st));
+  return rc;
+}
+
 int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                   const double* s0, const mcpx_out* o, mcpx::KernelArgs a, int nmax, hipStream_t st,
-                  mcpx_module* mod = nullptr) {
+                  mcpx_module* mod = nullptr, bool wg = false) {
+  if (wg) return launch_wg(d, theta, x0, y0, s0, o, a, nmax, st, mod);
   hipFunction_t nlf = nullptr;  // generated module: its kernel, launched by hipModuleLaunchKernel
   if (mod) {
-    const int rc = nl_function(mod, a.solver, &nlf);
+    const int rc = nl_function(mod, a.solver, false, &nlf);
     if (rc) return rc;
   }
   const int64_t CH = (int64_t)1 << 30;
-  const int n = d->n, m = d->m;
   for (int64_t b0 = 0; b0 < d->batch; b0 += CH) {
     const int64_t nb = std::min(CH, d->batch - b0);
-    a.theta = theta + b0 * d->theta_ld;
-    a.x0 = x0 ? x0 + b0 * n : nullptr;
-    a.y0 = y0 ? y0 + b0 * m : nullptr;
-    a.s0 = s0 ? s0 + b0 * m : nullptr;
-    a.x = o->x + b0 * n;
-    a.y = o->y + b0 * m;
-    a.s = o->s + b0 * m;
-    a.kkt_error = o->kkt_error + b0;
-    a.eps = o->eps + b0;
-    a.outer_iters = o->outer_iters + b0;
-    a.status = o->status + b0;
-    a.newton_iters = o->newton_iters ? o->newton_iters + b0 : nullptr;
-    a.active_mask = o->active_mask ? o->active_mask + b0 : nullptr;
-    a.alpha_trace = (o->alpha_trace && o->trace_len > 0) ? o->alpha_trace + b0 * (int64_t)o->trace_len * 2 : nullptr;
-    a.trace_len = o->alpha_trace ? o->trace_len : 0;
+    set_chunk(a, d, theta, x0, y0, s0, o, b0);
     if (mod) {
       void* params[] = {&a};
       HIP_TRY(hipModuleLaunchKernel(nlf, (unsigned)nb, 1, 1, 64, 1, 1, 0, st, params, nullptr));
@@ -257,7 +350,8 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   if (rc) return rc;
   mcpx::KernelArgs a;
   int nmax;
-  if ((rc = prepare(d, prm, &a, &nmax, mod))) return rc;
+  bool wg = false;
+  if ((rc = prepare(d, prm, &a, &nmax, mod, &wg))) return rc;
   const int n = d->n, m = d->m;
   if (m > 64 && o->active_mask) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
   DevBuf<double> th, dx0, dy0, ds0, x, y, s, kkt, eps;
@@ -282,7 +376,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   od.active_mask = am.p; od.alpha_trace = tr.p; od.trace_len = want_tr ? o->trace_len : 0;
   mcpx_desc dd = *d;
   dd.batch = nb;
-  if ((rc = launch_chunks(&dd, th.p, dx0.p, dy0.p, ds0.p, &od, a, nmax, nullptr, mod))) return rc;
+  if ((rc = launch_chunks(&dd, th.p, dx0.p, dy0.p, ds0.p, &od, a, nmax, nullptr, mod, wg))) return rc;
   HIP_TRY(hipDeviceSynchronize());
   auto back = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     return bytes ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
@@ -424,7 +518,8 @@ int solve_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta,
                       void* stream) {
   mcpx::KernelArgs a;
   int nmax;
-  int rc = prepare(d, prm, &a, &nmax, mod);
+  bool wg = false;
+  int rc = prepare(d, prm, &a, &nmax, mod, &wg);
   if (rc) return rc;
   if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
   if (d->batch == 0) return MCPX_OK;
@@ -433,7 +528,7 @@ int solve_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta,
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   if ((rc = check_device(dev))) return rc;
-  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod);
+  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod, wg);
 }
 
 // mcpx_solve_batch / mcpx_solve_batch_module: contiguous shards, one host thread per device.
@@ -488,6 +583,8 @@ void mcpx_default_params(mcpx_params* p) {
   p->min_stepsize = 1e-4;     // :48
   p->tau = 0.995;             // :127
   p->decay = 0.5;             // :127
+  p->linear_solver = MCPX_LINSOLVE_REDUCED;
+  p->kernel = MCPX_KERNEL_AUTO;
 }
 
 int64_t mcpx_theta_dim(int32_t family, int32_t n, int32_t m) {

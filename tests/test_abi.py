@@ -45,7 +45,7 @@ def test_library_has_gfx950_code_object():
 
 def test_version_and_constants():
     L = lib()
-    assert L.mcpx_version() == 10200
+    assert L.mcpx_version() == 10300
     for fam, (n, m) in [(0, (2, 2)), (0, (32, 16)), (1, (4, 8))]:
         assert L.mcpx_theta_dim(fam, n, m) == _abi.theta_dim(fam, n, m)
     assert L.mcpx_theta_dim(9, 2, 2) < 0 and L.mcpx_theta_dim(0, -1, 2) < 0
@@ -94,12 +94,15 @@ def test_param_errors(kw, code):
 
 
 def test_size_limits():
-    # reduced: n + m <= 64; dense: n + 2m <= 64
+    # one wave: reduced n + m <= 64, dense n + 2m <= 64 (MCPX_KERNEL_WAVE refuses beyond);
+    # workgroup kernels: n + 2m <= 768 (beyond: refused whatever the selector)
     desc = _abi.Desc(0, 40, 30, 0, 1, _abi.theta_dim(0, 40, 30))
-    assert _call(desc, np.zeros(_abi.theta_dim(0, 40, 30)), _abi.make_params()) == _abi.MCPX_EUNSUPPORTED
+    assert _call(desc, np.zeros(_abi.theta_dim(0, 40, 30)), _abi.make_params(kernel="wave")) == _abi.MCPX_EUNSUPPORTED
     desc = _abi.Desc(0, 32, 32, 0, 1, _abi.theta_dim(0, 32, 32))
     assert _call(desc, np.zeros(_abi.theta_dim(0, 32, 32)),
-                 _abi.make_params(linear_solver="dense")) == _abi.MCPX_EUNSUPPORTED
+                 _abi.make_params(linear_solver="dense", kernel="wave")) == _abi.MCPX_EUNSUPPORTED
+    desc = _abi.Desc(0, 400, 200, 0, 1, _abi.theta_dim(0, 400, 200))
+    assert _call(desc, np.zeros(_abi.theta_dim(0, 400, 200)), _abi.make_params()) == _abi.MCPX_EUNSUPPORTED
 
 
 def test_schur_needs_qp_family():

@@ -118,8 +118,10 @@ def test_generated_modules_compile(lane):
         path = mcp.nl.build_module()
         assert os.path.getsize(path) > 0
         blob = open(path, "rb").read()
-        for s, ok in mcp.nl.solvers().items():
-            assert (f"mcpx_nl_solve_{s}".encode() in blob) == ok, s
+        for s, ok in mcp.nl.solvers().items():  # symbol names are NUL-terminated in the ELF string table
+            assert (f"mcpx_nl_solve_{s}\0".encode() in blob) == ok, s
+        for s, ok in mcp.nl.wg_solvers().items():
+            assert (f"mcpx_nl_solve_{s}_wg\0".encode() in blob) == ok, s
 
 
 # ---------------------------------------------------------------- GPU
