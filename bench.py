@@ -68,6 +68,13 @@ def executed_flops(n: int, m: int, linear_solver: str) -> float:
     return f + (2.0 * n * n * m if linear_solver == "schur" else 0.0)
 
 
+def one_wave(n: int, m: int, linear_solver: str) -> bool:
+    """Whether the C ABI's default kernel selector (MCPX_KERNEL_AUTO) runs this QP size on
+    the one-wave register kernels (≤ 64 rows) rather than the workgroup-per-instance ones."""
+    lanes = n + 2 * m if linear_solver == "dense" else n + m
+    return solve_dim(n, m, linear_solver) <= 64 and lanes <= 64
+
+
 def roofline_bound(linear_solver: str) -> str:
     """What limits the solve kernels (PMC evidence): the register LU /
     Gauss-Jordan is FP64-VALU-issue-bound; θ traffic is ≤ 1/5 of HBM peak."""
@@ -219,16 +226,16 @@ def summary_statistics(step_s, count: int, success_rate: float) -> dict:
                    "unit": "s per solve (step time / instances per GPU)", "steps": len(per)}}
 
 
-def cpu_baseline(solve, count_avail: int, a, threads_all: int, label: str) -> dict:
+def cpu_baseline(solve, count_avail: int, a, threads_all: int, label: str, per_thread: int = 2048) -> dict:
     """Times the C oracle (the same algorithm as the kernel, oracle/ipm_oracle.c) on
     every CPU this process may use, on a bounded sample of the workload, plus one
     core alone.  `solve(k, threads)` solves the first k instances."""
-    solve(min(64, count_avail), threads_all)  # warm: library load, generated code compiled
-    S = min(count_avail, a.cpu_sample if a.cpu_sample > 0 else 2048 * threads_all)
+    solve(min(threads_all, count_avail), threads_all)  # warm: library load, generated code compiled
+    S = min(count_avail, a.cpu_sample if a.cpu_sample > 0 else per_thread * threads_all)
     t0 = time.perf_counter()
     r = solve(S, threads_all)
     dt = time.perf_counter() - t0
-    S1 = min(count_avail, max(64, S // max(threads_all, 1)))
+    S1 = min(count_avail, max(1, S // max(threads_all, 1)))
     t1 = time.perf_counter()
     solve(S1, 1)
     dt1 = time.perf_counter() - t1
@@ -345,7 +352,7 @@ def main_lane_change(a, world, rank, local, dist, pl):
     cfg = {"mode": "c4", "horizon": a.lane_change, "batch_per_gpu": B, "linear_solver": ls}
     key = f"c4_lane_t{a.lane_change}_b{B}"
     ev = evidence(key, cfg)
-    kernel = "mcpx_nl_solve_" + ls
+    kernel = "mcpx_nl_solve_" + ls + ("" if mcp.nl.solvers()[ls] else "_wg")
     rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
                   B * 8.0 * (mcp.nl.p + n + 2 * m + 2) + 12.0 * B, ev, kernel, "latency",
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system per Newton step) "
@@ -375,7 +382,8 @@ def main_lane_change(a, world, rank, local, dist, pl):
         th = a.cpu_threads or host_cpus()["nproc"]
         cb = cpu_baseline(lambda k, t: coracle.solve_batch_nl(mcp.nl, theta_host[:k], tol=a.tol, linear_solver=ls,
                                                               nthreads=t),
-                          B, a, th, "C oracle with the generated host G/H code (same algorithm and linear solver)")
+                          B, a, th, "C oracle with the generated host G/H code (same algorithm and linear solver)",
+                          per_thread=256 if a.lane_change <= 2 else 4)
         r = cb.pop("_result")
         cb["status_match"] = bool(np.array_equal(r["status"], out["status"][:len(r["status"])].cpu().numpy()))
         res["cpu_baseline"] = cb
@@ -471,7 +479,8 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     ev = evidence(key, cfg)
     p = n * n + m * n + m + n
     rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
-                  B * (8.0 * (p + n + 2 * m + 2) + 12.0), ev, "ipm_solve_kernel", roofline_bound(ls),
+                  B * (8.0 * (p + n + 2 * m + 2) + 12.0), ev,
+                  "ipm_solve_kernel" if one_wave(n, m, ls) else "ipm_wg_kernel_t", roofline_bound(ls),
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system, 2N^3/3+2N^2 per "
                   f"Newton step) x rank 0's own Newton counts / HIP-event time of the solve launch; executed = what "
                   f"the kernel performs ({ls}: LU of dim {NS}" + (" + 2n^2m Schur GEMM on fp64 MFMA" if ls == "schur"

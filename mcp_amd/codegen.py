@@ -9,14 +9,18 @@ csrc/ipm_nl_kernel.hpp into a code object the C ABI loads with
 same text, so the evaluation order — and with -ffp-contract=off every
 rounding — is identical on both sides.
 
-Generated functions (MCPX_NL_FN is `__device__` on the GPU, `static inline` in C):
+Generated functions (MCPX_NL_FN is `__device__` on the GPU, `static inline` in C)
+and tables (MCPX_NL_TABLE: `__constant__` on the GPU, `static const` in C):
 
   mcpx_nl_init(th, blk)      the Jacobian entries that do not depend on z
                              (θ-only and constant entries — the reference's
                              `constant_entries`, src/mcp.jl:111-112), once per
                              instance;
   mcpx_nl_eval(th, z, blk)   G, H and the z-dependent Jacobian entries at
-                             z = [x; y], once per Newton step.
+                             z = [x; y], once per Newton step;
+  mcpx_nl_qk_ptr / _idx      K(i): the structural nonzeros of row i of Q;
+  mcpx_nl_rj_ptr / _idx      J(k): the structural nonzeros of row k of R
+                             (the SCHUR elimination's sparse terms).
 
 Block layout of `blk` (doubles, column-major blocks like the affine family):
 
@@ -56,7 +60,7 @@ GEN_DIR = os.environ.get("MCPX_GEN_DIR") or os.path.join(HERE, "_gen")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
-GEN_VERSION = 2
+GEN_VERSION = 3
 _MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function")
 _MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "ipm_wg.h",
                 "ipm_wg_impl.hpp", "../../include/mcpx.h")
@@ -256,9 +260,25 @@ class NLSystem:
             lines.append(f"  blk[{idx}] = {pr(e)};")
         return lines
 
+    def structure(self):
+        """Structural nonzeros of Q = ∂G/∂y by rows (K(i): the k with Q_ik written by the
+        generated code, ascending) and of R = ∂H/∂x by rows (J(k), ascending), as CSR
+        (ptr, idx) pairs.  The SCHUR elimination forms S = (P + tol·I) − Q D⁻¹ R and
+        recovers δy from these terms only (oracle and kernels alike): structural zeros
+        are exact zeros, so they are never multiplied (as a sparse LU never touches them)."""
+        n, m = self.n, self.m
+        ents = {i for i, _ in self.const_entries} | {i for i, _ in self.var_entries}
+        qk = [[k for k in range(m) if self.OFF_Q + k * n + i in ents] for i in range(n)]
+        rj = [[j for j in range(n) if self.OFF_R + j * m + k in ents] for k in range(m)]
+        csr = lambda rows: ([0] + list(__import__("itertools").accumulate(len(r) for r in rows)),
+                            [x for r in rows for x in r])
+        return csr(qk), csr(rj)
+
     def _emit(self) -> str:
         init = self._block(self.const_entries, with_z=False)
         ev = self._block(self.var_entries + self.residuals, with_z=True)
+        (qp, qi), (rp, ri) = self.structure()
+        arr = lambda name, v: f"MCPX_NL_TABLE int32_t {name}[{max(len(v), 1)}] = {{{', '.join(map(str, v)) or '0'}}};"
         return "\n".join([
             "/* generated by mcp_amd/codegen.py — do not edit */",
             f"#define MCPX_NL_N {self.n}",
@@ -267,6 +287,13 @@ class NLSystem:
             f"#define MCPX_NL_HAS_S {int(self.has_s)}",
             f"#define MCPX_NL_SIZE {self.size}",
             f"#define MCPX_NL_NNZ {self.nnz}",
+            f"#define MCPX_NL_NNZ_Q {len(qi)}",
+            f"#define MCPX_NL_NNZ_R {len(ri)}",
+            "/* structural nonzeros: K(i) of Q row i, J(k) of R row k (CSR, ascending) */",
+            arr("mcpx_nl_qk_ptr", qp),
+            arr("mcpx_nl_qk_idx", qi),
+            arr("mcpx_nl_rj_ptr", rp),
+            arr("mcpx_nl_rj_idx", ri),
             "MCPX_NL_FN void mcpx_nl_init(const double* MCPX_NL_RESTRICT th, double* MCPX_NL_RESTRICT blk) {",
             "  (void)th;",
             "  (void)blk;",
@@ -288,6 +315,7 @@ class NLSystem:
             "#include <hip/hip_runtime.h>",
             "#define MCPX_NL_FN __device__ __forceinline__",
             "#define MCPX_NL_RESTRICT __restrict__",
+            "#define MCPX_NL_TABLE static __constant__ const",
             self.body,
             '#include "ipm_nl_kernel.hpp"',
             "",

@@ -20,7 +20,8 @@
 // z = [x; y; s], δz and F live in LDS too, so each linear solver has its own
 // lane ↔ row map:
 //   SCHUR   (∂H/∂y ≡ 0) δs, then δy eliminated exactly; lane i < n owns row i
-//           of S = (P + tol·I) − Q D⁻¹ R, D = tol + s/(y + tol)  (n ≤ 64, m ≤ 128);
+//           of S = (P + tol·I) − Q D⁻¹ R, D = tol + s/(y + tol)  (n ≤ 64, m ≤ 128),
+//           formed from Q's structural nonzeros only (oracle: the same terms);
 //   REDUCED δs eliminated; lanes [0, n+m) own the (n+m)-dim system;
 //   DENSE   lanes [0, n+2m) own the rows of ∇F + tol·I;
 // all three factor with the register LU with partial pivoting of the QP /
@@ -147,13 +148,12 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
           a[j] = lx ? v : 0.0;
         }
         double rhs = lx ? -Fs[i] : 0.0;
-        // unrolled ×2 so the uniform R·D⁻¹ row loads of k+1 overlap the fmas of k (same fma
-        // order per a[j]); C4: 13 % less time per Newton step.  ×5 keeps part of a[] in AGPRs
-        // and runs 29 % slower (it returned wrong iterates before the broadcast left the
-        // divergent region).
-#pragma unroll 2
-        for (int k = 0; k < m; ++k) {
-          const double q = lx ? -blk[OFF_Q + k * n + i] : 0.0;
+        // only Q's structural nonzeros of row i, K(i) ascending (mcpx_nl_qk_*, generated);
+        // lanes loop over their own list (at most 3 terms in the lane-change game, against m)
+        const int t0 = lx ? mcpx_nl_qk_ptr[i] : 0, t1 = lx ? mcpx_nl_qk_ptr[i + 1] : 0;
+        for (int t = t0; t < t1; ++t) {
+          const int k = mcpx_nl_qk_idx[t];
+          const double q = -blk[OFF_Q + k * n + i];
 #pragma unroll
           for (int j = 0; j < n; ++j) a[j] = fma(q, RDt[k * n + j], a[j]);
           rhs = fma(q, sTy[k], rhs);
@@ -168,7 +168,10 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
             const int k = lane + 64 * r;
             if (k < m) {
               double acc = sRy[k];
-              for (int j = 0; j < n; ++j) acc = fma(-blk[OFF_R + j * m + k], dzs[j], acc);
+              for (int t = mcpx_nl_rj_ptr[k]; t < mcpx_nl_rj_ptr[k + 1]; ++t) {  // R's structural nonzeros J(k)
+                const int j = mcpx_nl_rj_idx[t];
+                acc = fma(-blk[OFF_R + j * m + k], dzs[j], acc);
+              }
               const double dy = acc * sDi[k];
               dzs[n + k] = dy;
               dzs[n + m + k] = fma(-zs[n + m + k], dy, -Fs[n + m + k]) * sRw[k];
@@ -369,6 +372,10 @@ struct Gen {
   static constexpr bool HAS_S = nl::HAS_S;
   __device__ static void init(const double* th, double* blk) { mcpx_nl_init(th, blk); }
   __device__ static void eval(const double* th, const double* z, double* blk) { mcpx_nl_eval(th, z, blk); }
+  __device__ static const int32_t* qk_ptr() { return mcpx_nl_qk_ptr; }
+  __device__ static const int32_t* qk_idx() { return mcpx_nl_qk_idx; }
+  __device__ static const int32_t* rj_ptr() { return mcpx_nl_rj_ptr; }
+  __device__ static const int32_t* rj_idx() { return mcpx_nl_rj_idx; }
 };
 constexpr int NVW = imax(1, N);
 }  // namespace nl

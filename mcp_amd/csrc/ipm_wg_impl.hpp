@@ -27,7 +27,9 @@
 //     width that is not a multiple of 4 finishes on the VALU in the same order;
 //   * column-oriented back substitution, x_k = b_p / u_pk.
 // Residual, Jacobian rows, slack / y eliminations, line search and update follow
-// the oracle's solve_one() op for op (same fma chains, same order).
+// the oracle's solve_one() op for op (same fma chains, same order); the nonlinear
+// SCHUR elimination takes the terms of Q's and R's structural nonzeros only, as
+// the oracle does (the generated mcpx_nl_qk_* / mcpx_nl_rj_* tables).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -311,6 +313,10 @@ struct NoGen {
   static constexpr bool HAS_S = false;
   __device__ static void init(const double*, double*) {}
   __device__ static void eval(const double*, const double*, double*) {}
+  __device__ static const int32_t* qk_ptr() { return nullptr; }
+  __device__ static const int32_t* qk_idx() { return nullptr; }
+  __device__ static const int32_t* rj_ptr() { return nullptr; }
+  __device__ static const int32_t* rj_idx() { return nullptr; }
 };
 
 // Row i of F (src/mcp.jl:76-80) at z = zs, oracle family_row() op for op.
@@ -482,43 +488,26 @@ __device__ void solve_instances(const WgArgs& W) {
             RD[idx] = blk[GEN::OFF_R + j * m + k] * sD[k];
           }
           __syncthreads();
-          // S = (P + tol·I) + Σ_k (−Q_ik)(R_kj D_k⁻¹), k ascending, on the matrix cores
-          const int nt = (n + 15) / 16, wave = tid >> 6, lr = lane >> 4, lc = lane & 15;
-          const int mfull = m & ~3;
-          for (int t = wave; t < nt * nt; t += NWAVE) {
-            const int ti = t / nt, tj = t - ti * nt;
-            const int j = 16 * tj + lc;
-            d4 acc;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int i = 16 * ti + lr + 4 * e;
-              const double p = (i < n && j < n) ? blk[GEN::OFF_P + j * n + i] : 0.0;
-              acc[e] = (i == j) ? p + tol : p;
+          // S = (P + tol·I) + Σ_{k ∈ K(i)} (−Q_ik)(R_kj D_k⁻¹), k ascending over Q's structural
+          // nonzeros of row i (the oracle's terms), and rr_i = −F_Gi + Σ_{k ∈ K(i)} (−Q_ik) ty_k
+          const int32_t* qp = GEN::qk_ptr();
+          const int32_t* qi = GEN::qk_idx();
+          for (int idx = tid; idx < n * n; idx += WG) {
+            const int i = idx / n, j = idx - i * n;
+            double acc = blk[GEN::OFF_P + j * n + i];
+            if (i == j) acc += tol;
+            for (int t = qp[i]; t < qp[i + 1]; ++t) {
+              const int k = qi[t];
+              acc = fma(-blk[GEN::OFF_Q + k * n + i], RD[k * n + j], acc);
             }
-            const int ia = 16 * ti + lc;
-            for (int c = 0; c < mfull; c += 4) {
-              const int k = c + lr;
-              const double av = ia < n ? -blk[GEN::OFF_Q + k * n + ia] : 0.0;
-              const double bv = j < n ? RD[k * n + j] : 0.0;
-              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
-            for (int k = mfull; k < m; ++k) {  // m not a multiple of 4: the rest on the VALU, same order
-              const double bv = j < n ? RD[k * n + j] : 0.0;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int i = 16 * ti + lr + 4 * e;
-                acc[e] = fma(i < n ? -blk[GEN::OFF_Q + k * n + i] : 0.0, bv, acc[e]);
-              }
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int i = 16 * ti + lr + 4 * e;
-              if (i < n && j < n) Am[(int64_t)i * ld + j] = acc[e];
-            }
+            Am[(int64_t)i * ld + j] = acc;
           }
-          for (int i = tid; i < n; i += WG) {  // rr_i = −F_Gi + Σ_k (−Q_ik) ty_k
+          for (int i = tid; i < n; i += WG) {
             double acc = -Fs[i];
-            for (int k = 0; k < m; ++k) acc = fma(-blk[GEN::OFF_Q + k * n + i], sty[k], acc);
+            for (int t = qp[i]; t < qp[i + 1]; ++t) {
+              const int k = qi[t];
+              acc = fma(-blk[GEN::OFF_Q + k * n + i], sty[k], acc);
+            }
             Am[(int64_t)i * ld + n] = acc;
           }
         } else {
@@ -546,9 +535,14 @@ __device__ void solve_instances(const WgArgs& W) {
           break;
         }
         if constexpr (SCH) {  // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
+          const int32_t* rp = GEN::rj_ptr();
+          const int32_t* ri = GEN::rj_idx();
           for (int k = tid; k < m; k += WG) {
             double acc = sry[k];
-            for (int j = 0; j < n; ++j) acc = fma(-blk[GEN::OFF_R + j * m + k], dzs[j], acc);
+            for (int t = rp[k]; t < rp[k + 1]; ++t) {  // R's structural nonzeros J(k)
+              const int j = ri[t];
+              acc = fma(-blk[GEN::OFF_R + j * m + k], dzs[j], acc);
+            }
             const double dy = acc * sD[k];
             dzs[n + k] = dy;
             dzs[n + m + k] = fma(-zs[n + m + k], dy, -Fs[n + m + k]) * srw[k];

@@ -82,7 +82,8 @@ class OracleNL(C.Structure):
     """oracle_nl of ipm_oracle.c: the generated init/eval of one nonlinear MCP."""
 
     _fields_ = [("init", C.c_void_p), ("eval", C.c_void_p), ("p", C.c_int32), ("has_s", C.c_int32),
-                ("size", C.c_int32), ("pad_", C.c_int32)]
+                ("size", C.c_int32), ("pad_", C.c_int32), ("qk_ptr", C.c_void_p), ("qk_idx", C.c_void_p),
+                ("rj_ptr", C.c_void_p), ("rj_idx", C.c_void_p)]
 
 
 _GEN_DIR = os.path.join(_HERE, "_build", "gen")
@@ -99,11 +100,15 @@ def nl_lib(nl):
     if not os.path.exists(so):
         src = os.path.join(_GEN_DIR, f"nl_{nl.key}.c")
         with open(src, "w") as f:
-            f.write("#include <math.h>\n#define MCPX_NL_FN static inline\n#define MCPX_NL_RESTRICT restrict\n")
+            f.write("#include <math.h>\n#include <stdint.h>\n#define MCPX_NL_FN static inline\n"
+                    "#define MCPX_NL_RESTRICT restrict\n#define MCPX_NL_TABLE static const\n")
             f.write(nl.body)
             f.write("\nvoid oracle_nl_init(const double* th, double* blk) { mcpx_nl_init(th, blk); }\n"
                     "void oracle_nl_eval(const double* th, const double* z, double* blk) "
-                    "{ mcpx_nl_eval(th, z, blk); }\n")
+                    "{ mcpx_nl_eval(th, z, blk); }\n"
+                    "const int32_t* oracle_nl_table(int which) {\n"
+                    "  switch (which) { case 0: return mcpx_nl_qk_ptr; case 1: return mcpx_nl_qk_idx;\n"
+                    "    case 2: return mcpx_nl_rj_ptr; default: return mcpx_nl_rj_idx; }\n}\n")
         tmp = f"{so}.{os.getpid()}.tmp"
         subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
                         "-o", tmp, src, "-lm"], check=True)
@@ -138,8 +143,10 @@ def solve_batch_nl(nl, theta: np.ndarray, *, x0=None, y0=None, s0=None, params: 
               _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
               int(trace_len), 0)
     G = nl_lib(nl)
+    G.oracle_nl_table.restype = C.c_void_p
+    G.oracle_nl_table.argtypes = [C.c_int]
     spec = OracleNL(C.cast(G.oracle_nl_init, C.c_void_p).value, C.cast(G.oracle_nl_eval, C.c_void_p).value,
-                    nl.p, int(nl.has_s), nl.size, 0)
+                    nl.p, int(nl.has_s), nl.size, 0, *(G.oracle_nl_table(w) for w in range(4)))
     L = lib()
     L.oracle_solve_batch_nl.restype = C.c_int
     L.oracle_solve_batch_nl.argtypes = [C.POINTER(Desc), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -89,6 +89,9 @@ typedef struct oracle_nl {
   void (*init)(const double* th, double* blk);
   void (*eval)(const double* th, const double* z, double* blk);
   int32_t p, has_s, size, pad_;
+  /* structural nonzeros (mcp_amd/codegen.py NLSystem.structure): K(i) of row i of
+   * Q = ∂G/∂y and J(k) of row k of R = ∂H/∂x, CSR with ascending indices */
+  const int32_t *qk_ptr, *qk_idx, *rj_ptr, *rj_idx;
 } oracle_nl;
 
 /* doubles of the block array, the S block always included (zero when absent) */
@@ -386,6 +389,27 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           w->sry[k] = ry;
           w->sty[k] = ry * Di;
         }
+        if (nl) {
+          /* nonlinear family: only Q's structural nonzeros K(i) enter S and rr
+             (structural zeros are exact zeros; a sparse elimination never touches them) */
+          for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+              double acc = w->J[(size_t)i * N + j]; /* P_ij (+ tol) */
+              for (int t = nl->qk_ptr[i]; t < nl->qk_ptr[i + 1]; ++t) {
+                const int k = nl->qk_idx[t];
+                acc = fma(-w->J[(size_t)i * N + n + k], w->J[(size_t)(n + k) * N + j] * w->sD[k], acc);
+              }
+              w->Jr[(size_t)i * n + j] = acc;
+            }
+          for (int i = 0; i < n; ++i) {
+            double acc = w->b[i]; /* −F_Gi */
+            for (int t = nl->qk_ptr[i]; t < nl->qk_ptr[i + 1]; ++t) {
+              const int k = nl->qk_idx[t];
+              acc = fma(-w->J[(size_t)i * N + n + k], w->sty[k], acc);
+            }
+            w->b[i] = acc;
+          }
+        } else {
         for (int i = 0; i < n; ++i)
           for (int j = 0; j < n; ++j) {
             double acc = w->J[(size_t)i * N + j]; /* M_ij (+ tol) */
@@ -405,6 +429,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           for (int k = 0; k < m; ++k) acc = fma(-w->J[(size_t)i * N + n + k], w->sty[k], acc);
           w->b[i] = acc;
         }
+        }
         int spd_ok = 0;
         if (m_sym) {
           memcpy(w->Js, w->Jr, sizeof(double) * (size_t)n * n);
@@ -417,7 +442,14 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
         }
         for (int k = 0; k < m; ++k) {
           double acc = w->sry[k];
-          for (int j = 0; j < n; ++j) acc = fma(-w->J[(size_t)(n + k) * N + j], w->dz[j], acc);
+          if (nl) { /* R's structural nonzeros J(k) only */
+            for (int t = nl->rj_ptr[k]; t < nl->rj_ptr[k + 1]; ++t) {
+              const int j = nl->rj_idx[t];
+              acc = fma(-w->J[(size_t)(n + k) * N + j], w->dz[j], acc);
+            }
+          } else {
+            for (int j = 0; j < n; ++j) acc = fma(-w->J[(size_t)(n + k) * N + j], w->dz[j], acc);
+          }
           w->dz[n + k] = acc * w->sD[k];
         }
         for (int k = 0; k < m; ++k) {

@@ -184,18 +184,25 @@ def test_edge_inputs(gpu, oracle_lib, ls):
     assert empty["x"].shape == (0, n)
 
 
-def test_unsupported_sizes(gpu):
-    """Sizes outside the register-resident kernels are an error (MCPXError), not a silent fallback."""
+def test_unsupported_sizes(gpu, oracle_lib):
+    """Sizes outside what a kernel covers are an error (MCPXError), not a silent fallback:
+    beyond one wave with MCPX_KERNEL_WAVE, QP schur beyond one wave, KKT > 768.  In
+    between, the default selector runs the workgroup kernels (bit-exact, tests/test_wg.py)."""
     from mcp_amd import MCPXError
 
     th = generate_random_parameter(np.random.default_rng(0), 32, 32, 0.0, batch=2)
     with pytest.raises(MCPXError):
-        solve_batch(0, 32, 32, th, linear_solver="dense")  # n + 2m = 96
+        solve_batch(0, 32, 32, th, linear_solver="dense", kernel="wave")  # n + 2m = 96
+    got = solve_batch(0, 32, 32, th, linear_solver="dense", trace_len=TRACE)  # → workgroup kernel
+    assert_parity(got, oracle_lib.solve_batch(0, 32, 32, th, tol=1e-4, linear_solver="dense", trace_len=TRACE))
     th = generate_random_parameter(np.random.default_rng(0), 40, 30, 0.0, batch=2)
     with pytest.raises(MCPXError):
-        solve_batch(0, 40, 30, th)  # n + m = 70
+        solve_batch(0, 40, 30, th, kernel="wave")  # n + m = 70
     with pytest.raises(MCPXError):
         solve_batch(0, 40, 30, th, linear_solver="schur")
+    th = generate_random_parameter(np.random.default_rng(0), 400, 200, 0.0, batch=1)
+    with pytest.raises(MCPXError):
+        solve_batch(0, 400, 200, th, linear_solver="dense")  # n + 2m = 800 > 768
     from mcp_amd import _abi as abi
     tha = np.zeros((1, abi.theta_dim(1, 4, 4)))
     with pytest.raises(MCPXError):

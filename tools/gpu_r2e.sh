@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 2: GPU suite, large-KKT bench lines (lane change T=10, QP N=128/256 dense), MFMA evidence
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r2e
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 3
+timeout -k 10 300 python bench.py --lane-change 10 --global-batch 1024 --steps 2 --warmup 1 --cpu-sample 0 > $O/bench_c4_t10.json 2> $O/bench.err || exit 4
+timeout -k 10 300 python bench.py --n 64 --m 32 --linear-solver dense --global-batch 8192 --steps 3 --warmup 1 --cpu-sample 0 --host-runs 0 > $O/bench_qp_n128.json 2>> $O/bench.err || exit 5
+timeout -k 10 300 python bench.py --n 128 --m 64 --linear-solver dense --global-batch 2048 --steps 2 --warmup 1 --cpu-sample 0 --host-runs 0 > $O/bench_qp_n256.json 2>> $O/bench.err || exit 6
+timeout -k 10 300 python bench.py --n 48 --m 32 --linear-solver reduced --global-batch 8192 --steps 3 --warmup 1 --cpu-sample 0 --host-runs 0 > $O/bench_qp_n112_red.json 2>> $O/bench.err || exit 7
+bash tools/gpu_profile.sh c4t10 --lane-change 10 --global-batch 1024 --steps 2 --warmup 1 --cpu-sample 0 || exit 8
