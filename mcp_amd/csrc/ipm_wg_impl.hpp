@@ -133,11 +133,14 @@ __device__ __forceinline__ uint64_t pivot_key(double a) {
 // ---- blocked LU with partial pivoting (oracle lu_solve) --------------------
 //
 // A: ns × (ns + 1) row-major with stride ld, column ns = rhs; destroyed.
-// LDS: pan[NSMAX·NB], rem/ispiv/step/prow[NSMAX], x[NSMAX] (solution out).
+// x (LDS, ≥ ns): the solution, x[k] = δz_k.
 template <int NSMAX>
 struct LuShared {
-  double pan[NSMAX * NB];
-  int16_t rem[NSMAX];
+  double pan[NSMAX * NB];     // the panel, row q = remaining-list position q
+  double bb[NB];              // back substitution: rhs of the block's pivot rows
+  uint64_t key[2][NWAVE];     // pivot search, double-buffered by step parity
+  int32_t kpos[2][NWAVE];
+  int16_t rem[NSMAX];         // remaining rows, ascending
   int16_t step_of[NSMAX];
   int16_t prow[NSMAX];
   int16_t pivpos[NB];
@@ -145,50 +148,78 @@ struct LuShared {
   int32_t cnt[NWAVE];
 };
 
+// One pivot search per column with a single barrier: every thread owns the panel
+// rows q ≡ tid (mod 256) for the whole panel (their updates and pivot flags are
+// its own), so the only cross-thread data of a step are the 4 wave maxima and the
+// pivot row, both published before the barrier of the step's search.
 template <int NSMAX>
-__device__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuShared<NSMAX>& L, Scratch& sc) {
+__device__ __forceinline__ int panel_pivot(LuShared<NSMAX>& L, int r, int kk, int step) {
+  const int tid = threadIdx.x, wave = tid >> 6;
+  uint64_t key = 0;
+  int pos = -1;
+  for (int q = tid; q < r; q += WG)
+    if (!L.ispiv[q]) better(key, pos, pivot_key(L.pan[q * NB + kk]), q);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t k2 = shfl_xor_u64(key, o);
+    const int p2 = __shfl_xor(pos, o);
+    better(key, pos, k2, p2);
+  }
+  if ((tid & 63) == 0) {
+    L.key[step & 1][wave] = key;
+    L.kpos[step & 1][wave] = pos;
+  }
+  __syncthreads();
+  uint64_t k = L.key[step & 1][0];
+  int p = L.kpos[step & 1][0];
+#pragma unroll
+  for (int q = 1; q < NWAVE; ++q) better(k, p, L.key[step & 1][q], L.kpos[step & 1][q]);
+  return p;
+}
+
+template <int NSMAX>
+__device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuShared<NSMAX>& L) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < ns; i += WG) L.rem[i] = (int16_t)i;
   int r = ns;  // remaining rows (list length)
+  int step = 0;
   __syncthreads();
   for (int k0 = 0; k0 < ns; k0 += NB) {
     const int kb = min(NB, ns - k0);
-    // ---- stage the panel columns [k0, k0+kb) of the remaining rows ---------
-    for (int idx = tid; idx < r * NB; idx += WG) {
-      const int pos = idx / NB, kk = idx - pos * NB;
-      if (kk < kb) L.pan[idx] = A[(int64_t)L.rem[pos] * ld + k0 + kk];
+    // ---- stage the panel columns [k0, k0+kb) of the remaining rows (own rows) ----
+    for (int q = tid; q < r; q += WG) {
+      const double* src = A + (int64_t)L.rem[q] * ld + k0;
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk)
+        if (kk < kb) L.pan[q * NB + kk] = src[kk];
+      L.ispiv[q] = 0;
     }
-    for (int pos = tid; pos < r; pos += WG) L.ispiv[pos] = 0;
-    __syncthreads();
-    // ---- factor the panel column by column ----------------------------------
-    for (int kk = 0; kk < kb; ++kk) {
-      uint64_t key = 0;
-      int pos = -1;
-      for (int q = tid; q < r; q += WG)
-        if (!L.ispiv[q]) better(key, pos, pivot_key(L.pan[q * NB + kk]), q);
-      const int pp = wg_argmax(key, pos, sc);
+    // ---- factor the panel column by column (one barrier per column) -----------
+    for (int kk = 0; kk < kb; ++kk, ++step) {
+      const int pp = panel_pivot(L, r, kk, step);  // barrier inside: the previous update is visible
       const double piv = L.pan[pp * NB + kk];
       if (piv == 0.0) return false;  // the failed linear solve of src/solver.jl:84-88
-      if (tid == 0) {
+      if (tid == (pp & (WG - 1))) {  // the owner of the pivot row
         L.ispiv[pp] = 1;
         L.pivpos[kk] = (int16_t)pp;
         L.prow[k0 + kk] = L.rem[pp];
         L.step_of[L.rem[pp]] = (int16_t)(k0 + kk);
       }
-      __syncthreads();
       for (int q = tid; q < r; q += WG) {
-        if (L.ispiv[q]) continue;
+        if (q == pp || L.ispiv[q]) continue;
         double* row = L.pan + q * NB;
         const double l = row[kk] / piv;
         for (int jj = kk + 1; jj < kb; ++jj) row[jj] = fma(-l, L.pan[pp * NB + jj], row[jj]);
         row[kk] = l;  // a_ik of a remaining row is never read again: keep l_ik there
       }
-      __syncthreads();
     }
+    __syncthreads();
     // panel back to A: U11 in the pivot rows (their left part holds multipliers, never read)
-    for (int idx = tid; idx < r * NB; idx += WG) {
-      const int pos = idx / NB, kk = idx - pos * NB;
-      if (kk < kb) A[(int64_t)L.rem[pos] * ld + k0 + kk] = L.pan[idx];
+    for (int q = tid; q < r; q += WG) {
+      double* dst = A + (int64_t)L.rem[q] * ld + k0;
+#pragma unroll
+      for (int kk = 0; kk < NB; ++kk)
+        if (kk < kb) dst[kk] = L.pan[q * NB + kk];
     }
     // ---- U12: in-panel forward substitution of the pivot rows' trailing part -
     const int j_lo = k0 + kb;  // trailing columns j_lo .. ns (rhs = column ns)
@@ -211,41 +242,55 @@ __device__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuSh
     const int ncol = ns + 1 - j_lo;
     if (ncol > 0 && r > kb) {
       const int rt = (r + 15) / 16, ct = (ncol + 15) / 16;
-      const int kfull = kb & ~3;
       const int lr = lane >> 4, lc = lane & 15;
+      // U12 row of panel step kk: A + rem[pivpos[kk]]·ld (read from LDS where needed: kk is per lane)
+      auto urow = [&](int kk) { return (int64_t)L.rem[L.pivpos[kk]] * ld; };
       for (int t = wave; t < rt * ct; t += NWAVE) {
         const int ti = t / ct, tj = t - ti * ct;
         const int j = j_lo + 16 * tj + lc;
         const bool jin = j <= ns;
         d4 acc;
-        int rowp[4];
+        int64_t rowo[4];
         bool rin[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int pos = 16 * ti + lr + 4 * e;
           rin[e] = pos < r && !L.ispiv[pos < r ? pos : 0];
-          rowp[e] = pos < r ? L.rem[pos] : 0;
-          acc[e] = (rin[e] && jin) ? A[(int64_t)rowp[e] * ld + j] : 0.0;
+          rowo[e] = pos < r ? (int64_t)L.rem[pos] * ld : 0;
+          acc[e] = (rin[e] && jin) ? A[rowo[e] + j] : 0.0;
         }
         const int pa = 16 * ti + lc;  // A-fragment row of this lane
-        for (int c = 0; c < kfull; c += 4) {
-          const int kk = c + lr;
-          const double a = pa < r ? -L.pan[pa * NB + kk] : 0.0;
-          const double b = jin ? A[(int64_t)L.rem[L.pivpos[kk]] * ld + j] : 0.0;
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-        }
-        for (int kk = kfull; kk < kb; ++kk) {  // panel width not a multiple of 4: same order on the VALU
-          const double b = jin ? A[(int64_t)L.rem[L.pivpos[kk]] * ld + j] : 0.0;
+        if (kb == NB) {  // the common full panel: 4 K-chunks, loads hoisted ahead of the MFMA chain
+          double av[NB / 4], bv[NB / 4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int pos = 16 * ti + lr + 4 * e;
-            const double l = pos < r ? L.pan[pos * NB + kk] : 0.0;
-            acc[e] = fma(-l, b, acc[e]);
+          for (int c = 0; c < NB / 4; ++c) {
+            const int kk = 4 * c + lr;
+            av[c] = pa < r ? -L.pan[pa * NB + kk] : 0.0;
+            bv[c] = jin ? A[urow(kk) + j] : 0.0;
+          }
+#pragma unroll
+          for (int c = 0; c < NB / 4; ++c) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[c], bv[c], acc, 0, 0, 0);
+        } else {
+          const int kfull = kb & ~3;
+          for (int c = 0; c < kfull; c += 4) {
+            const int kk = c + lr;
+            const double a = pa < r ? -L.pan[pa * NB + kk] : 0.0;
+            const double b = jin ? A[urow(kk) + j] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+          }
+          for (int kk = kfull; kk < kb; ++kk) {  // width not a multiple of 4: same order on the VALU
+            const double b = jin ? A[urow(kk) + j] : 0.0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int pos = 16 * ti + lr + 4 * e;
+              const double l = pos < r ? L.pan[pos * NB + kk] : 0.0;
+              acc[e] = fma(-l, b, acc[e]);
+            }
           }
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (rin[e] && jin) A[(int64_t)rowp[e] * ld + j] = acc[e];
+          if (rin[e] && jin) A[rowo[e] + j] = acc[e];
       }
     }
     __syncthreads();
@@ -274,8 +319,12 @@ __device__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuSh
     r = base;
     __syncthreads();
   }
-  // ---- back substitution (column-oriented, oracle order) ----------------------
-  constexpr int RPT = (NSMAX + WG - 1) / WG;  // rows per thread
+  // ---- back substitution, blocked by 16 columns ---------------------------------
+  // Oracle order: row i takes fma(−u_ik, x_k, b_i) for k = ns−1 down to step_of(i)+1.
+  // Per block [k0, k0+16), descending: wave 0 solves the block's 16 pivot rows
+  // (each already updated by every later block) serially in registers, then every
+  // row of an earlier step takes the block's 16 updates, k descending.
+  constexpr int RPT = (NSMAX + WG - 1) / WG;  // rows per thread (rows i ≡ tid mod 256)
   double b[RPT];
   int st[RPT];
 #pragma unroll
@@ -284,21 +333,40 @@ __device__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuSh
     b[q] = i < ns ? A[(int64_t)i * ld + ns] : 0.0;
     st[q] = i < ns ? L.step_of[i] : 0x7fff;
   }
-  for (int k = ns - 1; k >= 0; --k) {
-    const int p = L.prow[k];
-    if ((p & (WG - 1)) == tid) {
-      double bp = 0.0;
+  const int nblk = (ns + NB - 1) / NB;
+  for (int blk = nblk - 1; blk >= 0; --blk) {
+    const int k0 = blk * NB, kb = min(NB, ns - k0);
+    // the block's pivot rows publish their rhs (final but for the block's own terms)
 #pragma unroll
-      for (int q = 0; q < RPT; ++q)
-        if (q == p / WG) bp = b[q];
-      x[k] = bp / A[(int64_t)p * ld + k];
+    for (int q = 0; q < RPT; ++q)
+      if (st[q] >= k0 && st[q] < k0 + kb) L.bb[st[q] - k0] = b[q];
+    __syncthreads();
+    if (wave == 0) {
+      // lane j (< kb) holds pivot row p_{k0+j}: its rhs and u_{p, k0..k0+kb-1}
+      const int j = lane < kb ? lane : 0;
+      const int64_t ro = (int64_t)L.prow[k0 + j] * ld + k0;
+      double bj = L.bb[j];
+      double uj[NB];
+#pragma unroll
+      for (int c = 0; c < NB; ++c) uj[c] = (c < kb) ? A[ro + c] : 0.0;
+#pragma unroll
+      for (int c = NB - 1; c >= 0; --c) {
+        if (c >= kb) continue;
+        const double t = bj / uj[c];  // lane c: x_{k0+c} = b_p / u_pk
+        const double xc = __shfl(t, c);
+        if (lane == c) x[k0 + c] = xc;
+        if (lane < c) bj = fma(-uj[c], xc, bj);
+      }
     }
     __syncthreads();
-    const double xk = x[k];
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int i = q * WG + tid;
-      if (i < ns && st[q] < k) b[q] = fma(-A[(int64_t)i * ld + k], xk, b[q]);
+      if (i >= ns || st[q] >= k0) continue;
+      const double* ur = A + (int64_t)i * ld + k0;
+#pragma unroll
+      for (int c = NB - 1; c >= 0; --c)
+        if (c < kb) b[q] = fma(-ur[c], x[k0 + c], b[q]);
     }
   }
   __syncthreads();
@@ -402,7 +470,7 @@ struct SolveShared {
 };
 
 template <int FAMILY, int SOLVER, int NVMAX, int NSMAX, class GEN>
-__device__ void solve_instances(const WgArgs& W) {
+__device__ __forceinline__ void solve_instances(const WgArgs& W) {
   constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR, RED = SOLVER == MCPX_LINSOLVE_REDUCED;
   constexpr bool NL = FAMILY == MCPX_FAMILY_NONLINEAR;
   static_assert(!SCH || (NL && !GEN::HAS_S), "the workgroup SCHUR path is the nonlinear family's (dH/dy = 0)");
@@ -530,7 +598,7 @@ __device__ void solve_instances(const WgArgs& W) {
         }
         __syncthreads();
         // ---- LU with partial pivoting (:83-88) ------------------------------------
-        if (!lu_solve<NSMAX>(Am, ld, ns, dzs, S.lu, S.sc)) {
+        if (!lu_solve<NSMAX>(Am, ld, ns, dzs, S.lu)) {
           status = 1;
           break;
         }
