@@ -62,10 +62,29 @@ def solve_dim(n: int, m: int, linear_solver: str) -> int:
 
 
 def executed_flops(n: int, m: int, linear_solver: str) -> float:
-    """FLOPs the kernel actually spends on the Newton linear solve per step: the LU of
-    the factored system, plus the Schur-complement GEMM (2n²m) for schur."""
-    f = lu_flops(solve_dim(n, m, linear_solver))
-    return f + (2.0 * n * n * m if linear_solver == "schur" else 0.0)
+    """FP64 FLOPs the QP kernels execute per Newton step (executed roofline):
+    the residual F (G rows n·(n+m) fmas, H rows m·n) plus the linear solve —
+      dense / reduced: LU with partial pivoting of the N = n+2m / n+m system (2N³/3 + 2N²);
+      schur: the Schur complement S = M + tol·I + Aᵀ D⁻¹ A on the matrix cores (2n²·4⌈m/4⌉,
+      K padded to the MFMA's 4), rr and δy (2nm each) and the pivot-free Gauss-Jordan
+      elimination of the SPD S, every other row updated at every step ((n−1)·n·(n+1)).
+    The one-wave kernels run every instance of the bench on these paths (M = PᵀP is
+    symmetric, S is SPD)."""
+    resid = 2.0 * (n * (n + m) + m * n)
+    if linear_solver == "schur":
+        return resid + 2.0 * n * n * 4 * ((m + 3) // 4) + 4.0 * n * m + (n - 1.0) * n * (n + 1.0)
+    return resid + lu_flops(solve_dim(n, m, linear_solver))
+
+
+def executed_flops_nl(nl, linear_solver: str) -> float:
+    """Same for a generated nonlinear module: the linear solve only (the generated G/H
+    evaluation is not counted) — schur: R·D⁻¹ (m·n products), S from Q's structural
+    nonzeros (2n per term), rr and δy over the Q / R patterns, LU of S."""
+    n, m = nl.n, nl.m
+    if linear_solver != "schur":
+        return lu_flops(solve_dim(n, m, linear_solver))
+    (qp, qi), (rp, ri) = nl.structure()
+    return m * n + 2.0 * n * len(qi) + 2.0 * len(qi) + 2.0 * len(ri) + lu_flops(n)
 
 
 def one_wave(n: int, m: int, linear_solver: str) -> bool:
@@ -353,12 +372,13 @@ def main_lane_change(a, world, rank, local, dist, pl):
     key = f"c4_lane_t{a.lane_change}_b{B}"
     ev = evidence(key, cfg)
     kernel = "mcpx_nl_solve_" + ls + ("" if mcp.nl.solvers()[ls] else "_wg")
-    rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
+    rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops_nl(mcp.nl, ls),
                   B * 8.0 * (mcp.nl.p + n + 2 * m + 2) + 12.0 * B, ev, kernel, "latency",
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system per Newton step) "
-                  f"x rank 0's own Newton counts / HIP-event kernel time; executed = what the kernel performs "
-                  f"({ls}: LU of dim {solve_dim(n, m, ls)}" + (" + 2n^2m Schur formation" if ls == "schur" else "")
-                  + "); bound: per-wave latency (PMC: waves stall on LDS/VALU dependencies, DESIGN.md §4)")
+                  f"x rank 0's own Newton counts / HIP-event kernel time; executed = the linear solve the kernel "
+                  f"performs ({ls}: LU of dim {solve_dim(n, m, ls)}" + (" + the Schur complement from Q's structural "
+                  "nonzeros" if ls == "schur" else "") + "); bound: per-wave latency (PMC: waves stall on LDS/VALU "
+                  "dependencies, DESIGN.md §4)")
     res = {
         "metric": "MCP solves/sec (lane-change trajectory game, generated nonlinear module)",
         "value": a.steps * pl["global_batch"] / elapsed, "unit": "solves/s", "n_gpus": world, "steps": a.steps,
@@ -450,14 +470,28 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     # reported beside `value`, never as it
     host = None
     if world == 1 and a.host_runs > 0 and not a.sens:
-        solve_batch(0, n, m, theta_host[:1024], tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
-        runs = []
-        for _ in range(a.host_runs):
-            t1 = time.perf_counter()
-            solve_batch(0, n, m, theta_host, tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
-            runs.append(time.perf_counter() - t1)
+        from mcp_amd.batch import pinned
+
+        def host_runs():
+            solve_batch(0, n, m, theta_host[:1024], tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
+            runs = []
+            for _ in range(a.host_runs):
+                t1 = time.perf_counter()
+                solve_batch(0, n, m, theta_host, tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
+                runs.append(time.perf_counter() - t1)
+            return runs
+
+        runs = host_runs()
+        t_reg = time.perf_counter()
+        with pinned(theta_host):
+            t_reg = time.perf_counter() - t_reg
+            runs_reg = host_runs()
         host = {"median_solves_per_s": B / float(np.median(runs)), "runs_s": runs,
-                "note": "mcpx_solve_batch on host numpy buffers: H->D theta, solve, D->H results"}
+                "registered_median_solves_per_s": B / float(np.median(runs_reg)), "registered_runs_s": runs_reg,
+                "register_s": t_reg, "theta_bytes": int(theta_host.nbytes),
+                "note": "mcpx_solve_batch on host numpy buffers (H->D theta, solve, D->H results; 2-stream chunked "
+                        "pipeline), median of runs after a warm-up; 'registered': theta page-locked once with "
+                        "mcpx_host_register (register_s, outside the runs)"}
     newton = out["newton_iters"].to(torch.float64).sum().item()
     solved = (out["status"] == 0).to(torch.float64).sum().item()
     (elapsed, kern_ms, vjp_ms), (newton_all, solved_all) = reduce_max_sum(
@@ -482,9 +516,10 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
                   B * (8.0 * (p + n + 2 * m + 2) + 12.0), ev,
                   "ipm_solve_kernel" if one_wave(n, m, ls) else "ipm_wg_kernel_t", roofline_bound(ls),
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system, 2N^3/3+2N^2 per "
-                  f"Newton step) x rank 0's own Newton counts / HIP-event time of the solve launch; executed = what "
-                  f"the kernel performs ({ls}: LU of dim {NS}" + (" + 2n^2m Schur GEMM on fp64 MFMA" if ls == "schur"
-                  else "") + "); bound: FP64 VALU issue (PMC, DESIGN.md §4); FP64 vector = matrix peak on MI355X; "
+                  f"Newton step) x rank 0's own Newton counts / HIP-event time of the solve launch; executed = the FP64 "
+                  f"work the kernel performs per step (residual + " + ("MFMA Schur complement + Gauss-Jordan of the "
+                  f"{NS}-dim SPD S" if ls == "schur" else f"LU of dim {NS}") + ", bench.executed_flops); "
+                  "bound: FP64 VALU issue (PMC, DESIGN.md §4); FP64 vector = matrix peak on MI355X; "
                   "frac_trace: same FLOPs over the committed rocprofv3 trace of this configuration and build")
     res = {
         "metric": METRIC,
@@ -517,15 +552,18 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     if a.sens:
         vbytes = B * 8 * (2 * p + 3 * N + 2 * N)  # θ read, ∂θ written, (x,y,s) + cotangents read
         vflops = B * lu_flops(N)
+        vexec = B * lu_flops(n + m)
         res["sensitivity"] = {
             "vjp_kernel_ms": vjp_ms, "solve_kernel_ms": kern_ms, "vjp_per_s": B / (vjp_ms * 1e-3),
             "vjp_failed": int((vstat != 0).sum().item()),
             "vjp_roofline": {"flops_per_launch": vflops, "achieved_tflops": vflops / (vjp_ms * 1e-3) / 1e12,
                              "frac_fp64": vflops / (vjp_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                             "executed_frac_fp64": vexec / (vjp_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                              "algorithmic_bytes": vbytes, "achieved_gbs": vbytes / (vjp_ms * 1e-3) / 1e9,
                              "frac_hbm": vbytes / (vjp_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                             "note": "one dense LU of the N-dim ∇F_zᵀ (2N³/3+2N²) per instance; bytes = θ read + "
-                                     "∂θ written + z and cotangents"},
+                             "note": "algorithmic: one dense LU of the N-dim ∇F_zᵀ (2N³/3+2N²) per instance; "
+                                     "executed: the LU of the slack-eliminated (n+m)-dim system the kernel "
+                                     "factors; bytes = θ read + ∂θ written + z and cotangents"},
         }
     if world == 1 and a.cpu_sample != 0:
         from oracle import coracle

@@ -46,6 +46,7 @@
 #ifndef MCPX_H
 #define MCPX_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -168,10 +169,20 @@ int mcpx_device_count(void);
  * Copies θ (and optional warm starts x0/y0/s0, each [B*n] / [B*m], NULL ⇒
  * the defaults x₀=0, y₀=1, s₀=1 of src/solver.jl:39-41) to `num_devices`
  * GPUs (0 ⇒ all visible), shards the batch contiguously, solves and copies
- * the outputs back.  Blocking. */
+ * the outputs back.  Blocking.  Per device the shard is pipelined in chunks on
+ * two streams (the upload of chunk c+1 overlaps the solve of chunk c); θ in a
+ * range registered with mcpx_host_register is read by DMA straight from the
+ * caller's pages, any other θ is staged by the HIP runtime. */
 int mcpx_solve_batch(const mcpx_desc* desc, const double* theta,
                      const double* x0, const double* y0, const double* s0,
                      const mcpx_params* prm, int num_devices, mcpx_out* out);
+
+/* Page-lock a caller-owned host range (hipHostRegister, all devices) so that the
+ * host-buffer calls read it by asynchronous DMA; optional, for long-lived θ
+ * batches.  The range must stay allocated until mcpx_host_unregister(ptr).
+ * MCPX_OK, MCPX_EINVAL (NULL / empty), MCPX_EHIP. */
+int mcpx_host_register(void* ptr, size_t bytes);
+int mcpx_host_unregister(void* ptr);
 
 /* Device-buffer batched solve on the current device: every pointer in the
  * call (theta, x0/y0/s0 and every mcpx_out array) is device memory.

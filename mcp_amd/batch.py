@@ -83,6 +83,25 @@ def solve_batch(family: int, n: int, m: int, theta, *, x0=None, y0=None, s0=None
     return r
 
 
+class pinned:
+    """Context manager that page-locks a host numpy array for the host-buffer calls
+    (mcpx_host_register / mcpx_host_unregister): θ is then read by asynchronous DMA
+    straight from it while earlier chunks solve.  For long-lived input batches."""
+
+    def __init__(self, array: np.ndarray):
+        if not (isinstance(array, np.ndarray) and array.flags.c_contiguous):
+            raise ValueError("pinned() needs a C-contiguous numpy array")
+        self.array = array
+
+    def __enter__(self):
+        check(lib().mcpx_host_register(self.array.ctypes.data, self.array.nbytes))
+        return self.array
+
+    def __exit__(self, *exc):
+        check(lib().mcpx_host_unregister(self.array.ctypes.data))
+        return False
+
+
 def alloc_device_outputs(B: int, n: int, m: int, device, trace_len: int = 0, newton: bool = True,
                          active: bool = True) -> dict:
     import torch

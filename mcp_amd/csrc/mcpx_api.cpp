@@ -341,10 +341,60 @@ struct DevBuf {
   hipError_t alloc(size_t count) { return count ? hipMalloc(&p, count * sizeof(T)) : hipSuccess; }
 };
 
-// One device's share of mcpx_solve_batch: instances [b0, b0+nb).
+// Device allocations of the host-buffer path come from the device's default
+// stream-ordered pool, kept warm across calls: the first call per device raises the
+// pool's release threshold, so freed blocks are reused by the next call instead of
+// returning to the driver (the caching a long-lived handle would give).
+int keep_pool_warm(int dev) {
+  static std::mutex mu;
+  static std::map<int, bool> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done[dev]) return MCPX_OK;
+  hipMemPool_t pool;
+  HIP_TRY(hipDeviceGetDefaultMemPool(&pool, dev));
+  uint64_t keep = UINT64_MAX;
+  HIP_TRY(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
+  done[dev] = true;
+  return MCPX_OK;
+}
+
+template <class T>
+struct AsyncBuf {  // stream-ordered device buffer, freed on the stream it was allocated on
+  T* p = nullptr;
+  hipStream_t st = nullptr;
+  hipError_t alloc(size_t count, hipStream_t s) {
+    st = s;
+    return count ? hipMallocAsync((void**)&p, count * sizeof(T), s) : hipSuccess;
+  }
+  ~AsyncBuf() { if (p) (void)hipFreeAsync(p, st); }
+};
+
+constexpr int kMaxHostStreams = 8;
+
+// Streams of the host-buffer pipeline: MCPX_HOST_STREAMS (A/B knob, 1..8, default 2).
+int host_streams() {
+  const char* e = std::getenv("MCPX_HOST_STREAMS");
+  const int v = e ? std::atoi(e) : 2;
+  return v < 1 ? 1 : (v > kMaxHostStreams ? kMaxHostStreams : v);
+}
+
+struct Streams {
+  hipStream_t s[kMaxHostStreams] = {};
+  ~Streams() {
+    for (auto& x : s)
+      if (x) (void)hipStreamDestroy(x);
+  }
+};
+
+// One device's share of mcpx_solve_batch: instances [b0, b0+nb), pipelined in
+// chunks of kChunk instances over S streams (default 2): θ (and warm starts) of
+// chunk c go up on stream c mod S while the previous chunks solve on the others;
+// the outputs land in whole-shard device buffers and come back once, after every
+// stream drained.
 int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                 const double* s0, const mcpx_params* prm, mcpx_out* o, int64_t b0, int64_t nb,
                 mcpx_module* mod = nullptr) {
+  constexpr int64_t kChunk = 8192;
   HIP_TRY(hipSetDevice(dev));
   int rc = check_device(dev);
   if (rc) return rc;
@@ -354,30 +404,58 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   if ((rc = prepare(d, prm, &a, &nmax, mod, &wg))) return rc;
   const int n = d->n, m = d->m;
   if (m > 64 && o->active_mask) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
-  DevBuf<double> th, dx0, dy0, ds0, x, y, s, kkt, eps;
-  DevBuf<int32_t> outer, status, newton;
-  DevBuf<uint64_t> am;
-  DevBuf<uint8_t> tr;
-  HIP_TRY(th.alloc((size_t)nb * d->theta_ld));
-  HIP_TRY(hipMemcpy(th.p, theta + b0 * d->theta_ld, sizeof(double) * (size_t)nb * d->theta_ld, hipMemcpyHostToDevice));
-  if (x0) { HIP_TRY(dx0.alloc((size_t)nb * n)); HIP_TRY(hipMemcpy(dx0.p, x0 + b0 * n, sizeof(double) * nb * n, hipMemcpyHostToDevice)); }
-  if (y0) { HIP_TRY(dy0.alloc((size_t)nb * m)); HIP_TRY(hipMemcpy(dy0.p, y0 + b0 * m, sizeof(double) * nb * m, hipMemcpyHostToDevice)); }
-  if (s0) { HIP_TRY(ds0.alloc((size_t)nb * m)); HIP_TRY(hipMemcpy(ds0.p, s0 + b0 * m, sizeof(double) * nb * m, hipMemcpyHostToDevice)); }
-  HIP_TRY(x.alloc((size_t)nb * n)); HIP_TRY(y.alloc((size_t)nb * m)); HIP_TRY(s.alloc((size_t)nb * m));
-  HIP_TRY(kkt.alloc(nb)); HIP_TRY(eps.alloc(nb)); HIP_TRY(outer.alloc(nb)); HIP_TRY(status.alloc(nb));
-  if (o->newton_iters) HIP_TRY(newton.alloc(nb));
-  if (o->active_mask) HIP_TRY(am.alloc(nb));
+  if ((rc = keep_pool_warm(dev))) return rc;
+  Streams ss;
+  const int S = host_streams();
+  for (int k = 0; k < S; ++k) HIP_TRY(hipStreamCreateWithFlags(&ss.s[k], hipStreamNonBlocking));
+  const int64_t ch = std::min(kChunk, nb);
+  const int64_t ld = d->theta_ld;
+  AsyncBuf<double> th[kMaxHostStreams], wx[kMaxHostStreams], wy[kMaxHostStreams], ws[kMaxHostStreams];
+  AsyncBuf<double> x, y, s, kkt, eps;
+  AsyncBuf<int32_t> outer, status, newton;
+  AsyncBuf<uint64_t> am;
+  AsyncBuf<uint8_t> tr;
+  hipStream_t s0st = ss.s[0];
+  for (int k = 0; k < S; ++k) {
+    HIP_TRY(th[k].alloc((size_t)ch * ld, ss.s[k]));
+    if (x0) HIP_TRY(wx[k].alloc((size_t)ch * n, ss.s[k]));
+    if (y0) HIP_TRY(wy[k].alloc((size_t)ch * m, ss.s[k]));
+    if (s0) HIP_TRY(ws[k].alloc((size_t)ch * m, ss.s[k]));
+  }
+  HIP_TRY(x.alloc((size_t)nb * n, s0st)); HIP_TRY(y.alloc((size_t)nb * m, s0st)); HIP_TRY(s.alloc((size_t)nb * m, s0st));
+  HIP_TRY(kkt.alloc(nb, s0st)); HIP_TRY(eps.alloc(nb, s0st)); HIP_TRY(outer.alloc(nb, s0st));
+  HIP_TRY(status.alloc(nb, s0st));
+  if (o->newton_iters) HIP_TRY(newton.alloc(nb, s0st));
+  if (o->active_mask) HIP_TRY(am.alloc(nb, s0st));
   const bool want_tr = o->alpha_trace && o->trace_len > 0;
-  if (want_tr) HIP_TRY(tr.alloc((size_t)nb * o->trace_len * 2));
-  if (want_tr) HIP_TRY(hipMemset(tr.p, 254, (size_t)nb * o->trace_len * 2));
-  mcpx_out od{};
-  od.x = x.p; od.y = y.p; od.s = s.p; od.kkt_error = kkt.p; od.eps = eps.p;
-  od.outer_iters = outer.p; od.status = status.p; od.newton_iters = newton.p;
-  od.active_mask = am.p; od.alpha_trace = tr.p; od.trace_len = want_tr ? o->trace_len : 0;
-  mcpx_desc dd = *d;
-  dd.batch = nb;
-  if ((rc = launch_chunks(&dd, th.p, dx0.p, dy0.p, ds0.p, &od, a, nmax, nullptr, mod, wg))) return rc;
-  HIP_TRY(hipDeviceSynchronize());
+  if (want_tr) {
+    HIP_TRY(tr.alloc((size_t)nb * o->trace_len * 2, s0st));
+    HIP_TRY(hipMemsetAsync(tr.p, 254, (size_t)nb * o->trace_len * 2, s0st));
+  }
+  hipEvent_t ready;  // the whole-shard allocations (stream 0) before the other streams use them
+  HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(ready, s0st));
+  for (int k = 1; k < S; ++k) HIP_TRY(hipStreamWaitEvent(ss.s[k], ready, 0));
+  (void)hipEventDestroy(ready);
+  for (int64_t c0 = 0, ci = 0; c0 < nb; c0 += ch, ++ci) {
+    const int k = (int)(ci % S);
+    hipStream_t st = ss.s[k];
+    const int64_t cn = std::min(ch, nb - c0), g0 = b0 + c0;
+    HIP_TRY(hipMemcpyAsync(th[k].p, theta + g0 * ld, sizeof(double) * (size_t)cn * ld, hipMemcpyHostToDevice, st));
+    if (x0) HIP_TRY(hipMemcpyAsync(wx[k].p, x0 + g0 * n, sizeof(double) * cn * n, hipMemcpyHostToDevice, st));
+    if (y0) HIP_TRY(hipMemcpyAsync(wy[k].p, y0 + g0 * m, sizeof(double) * cn * m, hipMemcpyHostToDevice, st));
+    if (s0) HIP_TRY(hipMemcpyAsync(ws[k].p, s0 + g0 * m, sizeof(double) * cn * m, hipMemcpyHostToDevice, st));
+    mcpx_out od{};
+    od.x = x.p + c0 * n; od.y = y.p + c0 * m; od.s = s.p + c0 * m; od.kkt_error = kkt.p + c0; od.eps = eps.p + c0;
+    od.outer_iters = outer.p + c0; od.status = status.p + c0; od.newton_iters = newton.p ? newton.p + c0 : nullptr;
+    od.active_mask = am.p ? am.p + c0 : nullptr;
+    od.alpha_trace = want_tr ? tr.p + c0 * (int64_t)o->trace_len * 2 : nullptr;
+    od.trace_len = want_tr ? o->trace_len : 0;
+    mcpx_desc dd = *d;
+    dd.batch = cn;
+    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, st, mod, wg))) return rc;
+  }
+  for (int k = 0; k < S; ++k) HIP_TRY(hipStreamSynchronize(ss.s[k]));
   auto back = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     return bytes ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
   };
@@ -436,7 +514,8 @@ int launch_sens(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, int nmax, const 
     a.theta_dot = tdot ? tdot + b0 * K * a.p : nullptr;
     a.out = out + (jvp ? b0 * K * N : b0 * a.p);
     a.status = status ? status + b0 : nullptr;
-    HIP_TRY(jvp ? mcpx::launch_jvp(nmax, a, nb, st) : mcpx::launch_vjp(nmax, a, nb, st));
+    // the VJP factors the slack-eliminated (n+m)-dim system, the JVP the full n+2m
+    HIP_TRY(jvp ? mcpx::launch_jvp(nmax, a, nb, st) : mcpx::launch_vjp(pick_nmax(n + m), a, nb, st));
   }
   return MCPX_OK;
 }
@@ -608,6 +687,18 @@ int mcpx_solve_batch_device(const mcpx_desc* d, const double* theta, const doubl
 int mcpx_solve_batch(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                      const double* s0, const mcpx_params* prm, int num_devices, mcpx_out* o) {
   return solve_host_impl(nullptr, d, theta, x0, y0, s0, prm, num_devices, o);
+}
+
+int mcpx_host_register(void* ptr, size_t bytes) {
+  if (!ptr || !bytes) return fail(MCPX_EINVAL, "mcpx_host_register: NULL pointer or empty range");
+  HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterPortable));
+  return MCPX_OK;
+}
+
+int mcpx_host_unregister(void* ptr) {
+  if (!ptr) return fail(MCPX_EINVAL, "mcpx_host_unregister: NULL pointer");
+  HIP_TRY(hipHostUnregister(ptr));
+  return MCPX_OK;
 }
 
 int mcpx_vjp_batch_device(const mcpx_desc* d, const double* theta, const double* x, const double* y,

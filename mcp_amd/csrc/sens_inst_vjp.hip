@@ -1,4 +1,4 @@
-// vjp_kernel instantiations (sens_kernel_impl.hpp) for NMAX ∈ {8,16,24,32,48,64} ≥ n + 2m,
+// vjp_kernel instantiations (sens_kernel_impl.hpp) for NMAX ∈ {8,16,24,32,48,64} ≥ n + m,
 // QP and affine families.  One translation unit so the build compiles it in parallel.
 #include "sens_kernel_impl.hpp"
 

@@ -7,8 +7,9 @@
 //
 //  * vjp_kernel — the rrule pullback (src/AutoDiff.jl:42-82):
 //        ∂θ = (∂z/∂θ)ᵀ g = −∇F_θᵀ λ,   ∇F_zᵀ λ = g = [∂l/∂x; ∂l/∂y; ∂l/∂s].
-//    Lane j owns row j of ∇F_zᵀ (= column j of ∇F_z) plus g_j; the register LU of
-//    the Newton step (lu_solve_rows, ipm_kernel_impl.hpp) solves for λ, which
+//    The s-rows of ∇F_zᵀ carry −1 at λh: eliminated exactly (λh = y⊙λc − gs),
+//    leaving an (n+m)-dim system; lane j owns its row j plus the rhs, the register
+//    LU of the Newton step (lu_solve_rows, ipm_kernel_impl.hpp) solves it, and λ
 //    goes to LDS with z; ∂θ is then written as coalesced rank-1 blocks
 //    (∂M = −λ_x xᵀ, ∂A_kj = λ_x,j y_k − λ_y,k x_j, ∂b = λ_y, ∂ϕ = λ_x for the QP
 //    family; −λ ⊗ z blocks for the affine family).
@@ -255,6 +256,51 @@ __device__ __forceinline__ void load_z(const SensArgs& A, int64_t inst, int ln, 
   zs[ln] = v;
 }
 
+// Row `ln` (< n + m) of the slack-eliminated ∇F_zᵀ system of the VJP (oracle
+// sens_one): unknowns u = [λx; λc]; λh = y⊙λc − gs follows from the −1 entries of
+// the s-rows.  Row j < n: [∇F_z[i][j] (i < n) | ∇F_z[n+k][j]·y_k]; row n+q:
+// [∇F_z[i][n+q] | ∇F_z[n+k][n+q]·y_k (+ s_q at k = q)]; rhs g_ln + Σ_k ∇F_z[n+k][ln]·gs_k.
+template <int NMAX, int FAMILY>
+__device__ __forceinline__ void vjp_reduced_row(const double* __restrict__ th, const double* zs, const double* gsv,
+                                                int ln, int n, int m, double (&a)[NMAX], double& rhs) {
+  const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m;
+  const bool lx = ln < n, lq = ln >= n && ln < n + m;
+  const int q = ln - n;
+  // column block of the G rows (∇F_z[i][ln], i < n) and of the H rows (∇F_z[n+k][ln], k < m)
+  const double* pg = th;  // stride sg over i
+  int sg = 0;
+  bool ng = false;
+  const double* ph = th;  // stride sh over k
+  int sh = 0;
+  bool uh = false;
+  if (lx) {
+    pg = th + (int64_t)ln * n; sg = 1;                                      // M[i,ln] / P[i,ln]
+    ph = th + (FAMILY == 0 ? nn : nn + nm) + (int64_t)ln * m; sh = 1; uh = true;  // A[k,ln] / R[k,ln]
+  }
+  if (lq) {
+    if (FAMILY == 0) { pg = th + nn + q; sg = m; ng = true; }              // −A[q,i]
+    else { pg = th + nn + (int64_t)q * n; sg = 1; }                         // Q[i,q]
+    if (FAMILY != 0) { ph = th + nn + 2 * nm + (int64_t)q * m; sh = 1; uh = true; }  // S[k,q]
+  }
+  const bool ug = lx || lq;
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) {
+    double v = 0.0;
+    if (j < n) {
+      const double t = pg[j * sg];
+      if (ug) v = ng ? -t : t;
+    } else if (j < n + m) {
+      const int k = j - n;
+      const double t = ph[k * sh];
+      if (uh) v = t * zs[n + k];          // ∇F_z[n+k][ln] · y_k
+      if (lq && k == q) v = v + zs[n + m + q];  // + s_q
+    }
+    a[j] = v;
+  }
+  if (gsv && uh)
+    for (int k = 0; k < m; ++k) rhs = fma(ph[k * sh], gsv[k], rhs);
+}
+
 template <int NMAX, int FAMILY>
 __global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
   __shared__ double zs[64];
@@ -266,16 +312,22 @@ __global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
   load_z(A, inst, ln, zs);
   __syncthreads();
   double a[NMAX];
-  const RowPattern P = row_pattern<FAMILY, true>(zs, ln, n, m);
-  assemble_pattern_row<NMAX>(th, P, n, m, a);
   double g = 0.0;  // ∂l/∂z_ln (NULL cotangent block = ZeroTangent)
   if (ln < n) { if (A.gx) g = A.gx[inst * n + ln]; }
   else if (ln < n + m) { if (A.gy) g = A.gy[inst * m + (ln - n)]; }
-  else if (ln < N) { if (A.gs) g = A.gs[inst * m + (ln - n - m)]; }
+  const double* gsv = A.gs ? A.gs + inst * m : nullptr;
+  vjp_reduced_row<NMAX, FAMILY>(th, zs, gsv, ln, n, m, a, g);
   double l = 0.0;
-  const bool ok = lu_solve_rows<NMAX>(a, g, N, ln, l);
-  lam[ln] = ok ? l : __builtin_nan("");
+  const bool ok = lu_solve_rows<NMAX>(a, g, n + m, ln, l);
+  // [λx; λc] → [λx; λh], λh_q = y_q·λc_q − gs_q
+  double lv = l;
+  if (ln >= n && ln < n + m) {
+    const int q = ln - n;
+    lv = gsv ? fma(zs[n + q], l, -gsv[q]) : zs[n + q] * l;
+  }
+  lam[ln] = ok ? lv : __builtin_nan("");
   __syncthreads();
+  (void)N;
   if (A.status && ln == 0) A.status[inst] = ok ? 0 : 1;
   double* o = A.out + inst * A.p;
   const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;

@@ -628,7 +628,8 @@ int oracle_solve_batch_nl(const mcpx_desc* d, const double* theta, const double*
  * ∂z/∂θ = −(∇F_z)⁻¹ ∇F_θ at the returned (x, y, s), ∇F_z WITHOUT tol·I
  * (src/AutoDiff.jl:18-40; Appendix A.10 of SURVEY.md).  The reference solves
  * with a column-pivoted QR of −∇F_z (LAPACK geqp3, :39); this restatement uses
- * lu_solve() above on ∇F_z (JVP) or ∇F_zᵀ (VJP): equal for nonsingular ∇F_z up
+ * lu_solve() above on ∇F_z (JVP) or on the slack-eliminated (n+m)-dim rows of
+ * ∇F_zᵀ (VJP, exact elimination through the −1 entries): equal for nonsingular ∇F_z up
  * to rounding (tests/test_oracle.py cross-checks against a numpy pivoted-QR
  * restatement, oracle/ipm_ref.py).  Exactly singular ⇒ status 1, NaN outputs.
  * ====================================================================== */
@@ -719,18 +720,41 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
   const double nanv = __builtin_nan("");
   int failed = 0;
   if (!j->jvp) {
-    /* rrule pullback, src/AutoDiff.jl:59-76: ∇F_zᵀ λ = g, ∂θ = −∇F_θᵀ λ */
+    /* rrule pullback, src/AutoDiff.jl:59-76: ∇F_zᵀ λ = g, ∂θ = −∇F_θᵀ λ, solved on the
+       slack-eliminated (n+m) system.  Row n+m+r of ∇F_zᵀ is [−1 at λh_r, y_r at λc_r] = gs_r:
+       its −1 eliminates λh_r = y_r·λc_r − gs_r exactly (no division), leaving for
+       u = [λx; λc]:
+         row j < n:  Σ_i ∇F_z[i][j] λx_i + Σ_k (∇F_z[n+k][j]·y_k) λc_k = gx_j + Σ_k ∇F_z[n+k][j] gs_k
+         row n+q:    Σ_i ∇F_z[i][n+q] λx_i + Σ_k (∇F_z[n+k][n+q]·y_k) λc_k (+ s_q at k = q) = gy_q
+                     + Σ_k ∇F_z[n+k][n+q] gs_k
+       (gs = NULL: the Σ gs chains are skipped), factored by lu_solve like the solver's
+       REDUCED Newton system.  The GPU's vjp_kernel forms the same rows. */
     jacobian_z(d->family, n, m, th, w->z, w->J);
-    for (int r = 0; r < N; ++r)
-      for (int c = 0; c < N; ++c) w->JT[(size_t)r * N + c] = w->J[(size_t)c * N + r];
-    for (int i = 0; i < n; ++i) w->b[i] = j->gx ? j->gx[b * n + i] : 0.0;
-    for (int k = 0; k < m; ++k) {
-      w->b[n + k] = j->gy ? j->gy[b * m + k] : 0.0;
-      w->b[n + m + k] = j->gs ? j->gs[b * m + k] : 0.0;
+    const int Nr = n + m;
+    const double* yv = w->z + n;
+    const double* sv = w->z + n + m;
+    for (int r = 0; r < Nr; ++r) {
+      double* row = w->JT + (size_t)r * Nr;
+      for (int i = 0; i < n; ++i) row[i] = w->J[(size_t)i * N + r];
+      for (int k = 0; k < m; ++k) {
+        double v = w->J[(size_t)(n + k) * N + r] * yv[k];
+        if (r == n + k) v = v + sv[k];
+        row[n + k] = v;
+      }
+      double acc = r < n ? (j->gx ? j->gx[b * n + r] : 0.0) : (j->gy ? j->gy[b * m + (r - n)] : 0.0);
+      if (j->gs)
+        for (int k = 0; k < m; ++k) acc = fma(w->J[(size_t)(n + k) * N + r], j->gs[b * m + k], acc);
+      w->b[r] = acc;
     }
-    failed = lu_solve(N, w->JT, w->b, w->dz, w->rem, w->step, w->prow);
-    if (failed)
+    failed = lu_solve(Nr, w->JT, w->b, w->dz, w->rem, w->step, w->prow);
+    if (failed) {
       for (int i = 0; i < N; ++i) w->dz[i] = nanv;
+    } else {  /* [λx; λc] → [λx; λh]: λh_k = y_k·λc_k − gs_k */
+      for (int k = 0; k < m; ++k) {
+        const double lc = w->dz[n + k];
+        w->dz[n + k] = j->gs ? fma(yv[k], lc, -j->gs[b * m + k]) : yv[k] * lc;
+      }
+    }
     const double* lx = w->dz;      /* λ of the G rows */
     const double* ly = w->dz + n;  /* λ of the H − s rows */
     const double* x = w->z;

@@ -118,3 +118,10 @@ def test_no_device_is_an_error_not_a_fallback():
     assert _call(desc, np.zeros(16), _abi.make_params()) == _abi.MCPX_ENODEV
     with pytest.raises(MCPXError):
         check(_abi.MCPX_ENODEV)
+
+
+def test_host_register_argument_errors():
+    assert lib().mcpx_host_register(None, 16) == _abi.MCPX_EINVAL
+    buf = np.zeros(4)
+    assert lib().mcpx_host_register(buf.ctypes.data, 0) == _abi.MCPX_EINVAL
+    assert lib().mcpx_host_unregister(None) == _abi.MCPX_EINVAL

@@ -28,8 +28,12 @@ def test_solve_dims_and_executed_flops():
     assert bench.solve_dim(32, 16, "dense") == 64
     assert bench.solve_dim(32, 16, "reduced") == 48
     assert bench.solve_dim(32, 16, "schur") == 32
-    assert bench.executed_flops(32, 16, "schur") == bench.lu_flops(32) + 2 * 32 * 32 * 16
-    assert bench.executed_flops(32, 16, "dense") == bench.lu_flops(64)
+    resid = 2 * (32 * 48 + 16 * 32)
+    # Gauss-Jordan of the SPD S: every other row at every step, (n-1)·n·(n+1) = 32,736 at n = 32
+    assert bench.executed_flops(32, 16, "schur") == resid + 2 * 32 * 32 * 16 + 4 * 32 * 16 + 31 * 32 * 33
+    assert bench.executed_flops(32, 16, "dense") == resid + bench.lu_flops(64)
+    # m = 15: residual −2·(32 + 32), rr/δy −4·32, the Schur GEMM's K stays padded to 16
+    assert bench.executed_flops(32, 16, "schur") - bench.executed_flops(32, 15, "schur") == 256
     assert bench.roofline_bound("schur") == "valu"
 
 

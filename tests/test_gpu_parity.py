@@ -253,3 +253,22 @@ def test_full_size_properties(gpu, oracle_lib, ls):
     sub["active_mask"] = sub["active_mask"].astype(np.uint64).reshape(-1, 1)
     sub["alpha_trace"] = np.zeros((len(idx), 0, 2), np.uint8)
     assert_parity(sub, ref)
+
+
+def test_host_pipeline_chunks_and_registration(gpu, oracle_lib):
+    """The host-buffer path pipelines a shard in chunks of 8,192 on two streams: a
+    ragged 3-chunk batch with warm starts, α traces and active sets equals the
+    oracle, and equals itself with θ page-locked (mcpx_host_register)."""
+    from mcp_amd.batch import pinned
+
+    n, m, B = 6, 4, 8192 * 2 + 777
+    th = generate_random_parameter(np.random.default_rng(21), n, m, 0.0, batch=B)
+    rng = np.random.default_rng(22)
+    x0, y0 = 0.1 * rng.standard_normal((B, n)), rng.uniform(0.5, 1.5, (B, m))
+    got = solve_batch(0, n, m, th, x0=x0, y0=y0, tol=1e-6, trace_len=64, linear_solver="schur")
+    ref = oracle_lib.solve_batch(0, n, m, th, x0=x0, y0=y0, tol=1e-6, trace_len=64, linear_solver="schur",
+                                 nthreads=8)
+    assert_parity(got, ref)
+    with pinned(th):
+        again = solve_batch(0, n, m, th, x0=x0, y0=y0, tol=1e-6, trace_len=64, linear_solver="schur")
+    assert_parity(again, ref)
