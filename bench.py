@@ -43,6 +43,7 @@ sys.path.insert(0, ROOT)
 METRIC = "MCP solves/sec (batched QP-KKT, n=64) at 1/2/4/8 GPUs; % LU roofline"
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+XCDS, SIMDS = 8, 256 * 4  # MI355X: 8 XCDs, 256 CUs × 4 SIMDs
 # rocprofv3 evidence of this round's kernels (tools/gpu_profile.sh + tools/prof_summary.py)
 PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
 DEFAULT_GLOBAL = {"c3": 65536, "c5": 4096, "c4": 1024}
@@ -323,6 +324,12 @@ def roofline(kern_ms: float, flops_launch: float, exec_flops_launch: float, alg_
                  trace_source=tr["_source"])
     if traffic:
         r["traffic_over_algorithmic"] = traffic / alg_bytes
+    p = ev.get("pmc") or {}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in p and p.get("GRBM_GUI_ACTIVE"):
+        # rocprofv3's MfmaUtil: Σ MFMA-busy SIMD-cycles / (GPU-active cycles × SIMDs); the per-dispatch
+        # GRBM_GUI_ACTIVE of the CSV is the sum over the 8 XCDs, hence / 8
+        r["mfma_util"] = p["SQ_VALU_MFMA_BUSY_CYCLES"] / (p["GRBM_GUI_ACTIVE"] / XCDS * SIMDS)
+        r["mfma_tflops_pmc"] = p.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) * 512 / (kern_ms * 1e-3) / 1e12
     return r
 
 
