@@ -60,8 +60,9 @@ GEN_DIR = os.environ.get("MCPX_GEN_DIR") or os.path.join(HERE, "_gen")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
-GEN_VERSION = 3
-_MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function")
+GEN_VERSION = 4
+_MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function",
+                 "-mllvm", "-amdgpu-mfma-vgpr-form=1")
 _MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "ipm_wg.h",
                 "ipm_wg_impl.hpp", "../../include/mcpx.h")
 WG_LDS_LIMIT = 160 * 1024 - 2048  # MCPX_NL_WG_LIMIT of csrc/ipm_nl_kernel.hpp
@@ -243,20 +244,38 @@ class NLSystem:
 
     # ---- emission ------------------------------------------------------------
     def _block(self, entries, with_z: bool) -> list:
+        """Straight-line C for `entries` after common-subexpression elimination.  Each
+        CSE temporary is emitted right before the first statement that needs it
+        (dependency order kept), not all at the top: at horizon T = 10 the
+        all-at-the-top form kept ~170 temporaries and every z load live at once, and
+        the kernel it is inlined into spilled (512 registers + scratch)."""
         sp = _sp()
         names = {t: f"th[{k}]" for k, t in enumerate(self.ts)}
-        if with_z:
-            names.update({x: f"z[{j}]" for j, x in enumerate(self.xs)})
-            names.update({y: f"z[{self.n + k}]" for k, y in enumerate(self.ys)})
+        if with_z:  # MCPX_NL_Z: a fresh load per use on the GPU (see hip_source), plain z[j] in C
+            names.update({x: f"MCPX_NL_Z({j})" for j, x in enumerate(self.xs)})
+            names.update({y: f"MCPX_NL_Z({self.n + k})" for k, y in enumerate(self.ys)})
         if not entries:
             return []
         reps, red = sp.cse([e for _, e in entries], symbols=sp.numbered_symbols("c"), order="canonical")
         pr = _Printer(names)
-        lines = []
-        for sym, e in reps:
-            lines.append(f"  const double {sym} = {pr(e)};")
-            names[sym] = str(sym)
+        rep_of = {sym: e for sym, e in reps}
+        order = {sym: i for i, (sym, _) in enumerate(reps)}
+        emitted, lines = set(), []
+
+        def need(e):  # CSE temporaries e depends on, transitively, in definition order
+            out, stack = set(), [e]
+            while stack:
+                for f in stack.pop().free_symbols:
+                    if f in rep_of and f not in out and f not in emitted:
+                        out.add(f)
+                        stack.append(rep_of[f])
+            return sorted(out, key=order.get)
+
         for (idx, _), e in zip(entries, red):
+            for sym in need(e):
+                lines.append(f"  const double {sym} = {pr(rep_of[sym])};")
+                names[sym] = str(sym)
+                emitted.add(sym)
             lines.append(f"  blk[{idx}] = {pr(e)};")
         return lines
 
@@ -316,6 +335,9 @@ class NLSystem:
             "#define MCPX_NL_FN __device__ __forceinline__",
             "#define MCPX_NL_RESTRICT __restrict__",
             "#define MCPX_NL_TABLE static __constant__ const",
+            "// z is read afresh at every use (LDS, cheap): kept in registers from its first use, the",
+            "// ~450 z values of a T = 10 game made the kernel spill",
+            "#define MCPX_NL_Z(j) (((const volatile double*)z)[j])",
             self.body,
             '#include "ipm_nl_kernel.hpp"',
             "",

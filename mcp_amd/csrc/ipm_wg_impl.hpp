@@ -476,7 +476,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
   static_assert(!SCH || (NL && !GEN::HAS_S), "the workgroup SCHUR path is the nonlinear family's (dH/dy = 0)");
   __shared__ SolveShared<NVMAX, NSMAX> S;
   const KernelArgs& a = W.k;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = a.n, m = a.m, N = n + 2 * m;
   const int ns = SCH ? n : (RED ? n + m : N);
   const int ld = W.ld;
@@ -551,17 +551,15 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
             sty[k] = ry * Di;
           }
           __syncthreads();
-          for (int idx = tid; idx < m * n; idx += WG) {  // R_kj · D_k⁻¹, row k
-            const int k = idx / n, j = idx - k * n;
-            RD[idx] = blk[GEN::OFF_R + j * m + k] * sD[k];
-          }
+          for (int k = wave; k < m; k += NWAVE)  // R_kj · D_k⁻¹, row k (wave per row, lanes over j)
+            for (int j = lane; j < n; j += 64) RD[k * n + j] = blk[GEN::OFF_R + j * m + k] * sD[k];
           __syncthreads();
           // S = (P + tol·I) + Σ_{k ∈ K(i)} (−Q_ik)(R_kj D_k⁻¹), k ascending over Q's structural
           // nonzeros of row i (the oracle's terms), and rr_i = −F_Gi + Σ_{k ∈ K(i)} (−Q_ik) ty_k
           const int32_t* qp = GEN::qk_ptr();
           const int32_t* qi = GEN::qk_idx();
-          for (int idx = tid; idx < n * n; idx += WG) {
-            const int i = idx / n, j = idx - i * n;
+          for (int i = wave; i < n; i += NWAVE)
+            for (int j = lane; j < n; j += 64) {  // wave per row i, lanes over j
             double acc = blk[GEN::OFF_P + j * n + i];
             if (i == j) acc += tol;
             for (int t = qp[i]; t < qp[i + 1]; ++t) {
@@ -579,9 +577,8 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
             Am[(int64_t)i * ld + n] = acc;
           }
         } else {
-          const int w1 = ns + 1;
-          for (int idx = tid; idx < ns * w1; idx += WG) {
-            const int i = idx / w1, j = idx - i * w1;
+          for (int i = wave; i < ns; i += NWAVE)
+            for (int j = lane; j <= ns; j += 64) {  // wave per row i, lanes over the ns + 1 columns
             double v;
             if (j < ns) {
               v = jac<FAMILY, GEN>(th, blk, zs, n, m, i, j);

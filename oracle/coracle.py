@@ -101,7 +101,8 @@ def nl_lib(nl):
         src = os.path.join(_GEN_DIR, f"nl_{nl.key}.c")
         with open(src, "w") as f:
             f.write("#include <math.h>\n#include <stdint.h>\n#define MCPX_NL_FN static inline\n"
-                    "#define MCPX_NL_RESTRICT restrict\n#define MCPX_NL_TABLE static const\n")
+                    "#define MCPX_NL_RESTRICT restrict\n#define MCPX_NL_TABLE static const\n"
+                    "#define MCPX_NL_Z(j) (z[j])\n")
             f.write(nl.body)
             f.write("\nvoid oracle_nl_init(const double* th, double* blk) { mcpx_nl_init(th, blk); }\n"
                     "void oracle_nl_eval(const double* th, const double* z, double* blk) "
