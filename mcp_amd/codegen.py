@@ -58,6 +58,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 GEN_DIR = os.environ.get("MCPX_GEN_DIR") or os.path.join(HERE, "_gen")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# x + y entries above which the generated code re-reads z per use (register pressure)
+Z_VOLATILE_ABOVE = int(os.environ.get("MCPX_NL_Z_VOLATILE_ABOVE", "128"))
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
 GEN_VERSION = 4
@@ -335,9 +337,12 @@ class NLSystem:
             "#define MCPX_NL_FN __device__ __forceinline__",
             "#define MCPX_NL_RESTRICT __restrict__",
             "#define MCPX_NL_TABLE static __constant__ const",
-            "// z is read afresh at every use (LDS, cheap): kept in registers from its first use, the",
-            "// ~450 z values of a T = 10 game made the kernel spill",
-            "#define MCPX_NL_Z(j) (((const volatile double*)z)[j])",
+            "// z lives in LDS (the address space makes its reads ds_read; a generic pointer compiled",
+            "// them to flat loads).  Large problems read it afresh at every use (volatile): kept in",
+            "// registers from its first use, the ~450 z values of a T = 10 game made the kernel spill;",
+            "// small ones let the compiler batch the loads.",
+            "#define MCPX_NL_Z(j) (((const " + ("volatile " if self.n + self.m > Z_VOLATILE_ABOVE else "")
+            + "__attribute__((address_space(3))) double*)z)[j])",
             self.body,
             '#include "ipm_nl_kernel.hpp"',
             "",

@@ -37,15 +37,14 @@
 // A DPP read of a VGPR needs 2 wait states after a VALU write of it, and hipcc
 // does not pad hazards whose reader is inside an asm statement: a register copy
 // it places right before a DPP fmac would feed the fmac a stale source
-// (tools/check_dpp_hazards.py finds them in the .s).  MCPX_DPP_PAD pads each
-// DPP fmac with the 2 states.
+// (tools/check_dpp_hazards.py finds them in the .s, and the build refuses such
+// an object).  The DPP fmacs of the Gauss-Jordan take a PAD template flag: the
+// compile-time-(n, m) kernels run unpadded (the checker passes them; the pads
+// cost 2-3 % at C3, profiles/r02/ab_c3_pad_waves.jsonl), the generic kernels,
+// where the allocator does place copies right before the asm, keep an
+// s_nop 1 per fmac.  MCPX_DPP_PAD_ON=1 pads every kernel.
 #ifndef MCPX_DPP_PAD_ON
-#define MCPX_DPP_PAD_ON 1
-#endif
-#if MCPX_DPP_PAD_ON
-#define MCPX_DPP_PAD "s_nop 1\n"
-#else
-#define MCPX_DPP_PAD ""
+#define MCPX_DPP_PAD_ON 0
 #endif
 
 // Waves per SIMD the register allocator targets in the SCHUR fast pass (A/B knob).
@@ -293,43 +292,11 @@ __device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, in
   }
 }
 
-// Pivot-free Gauss-Jordan elimination of [S | rhs] for symmetric positive
-// definite S (the SCHUR complement when M is symmetric): pivot k is lane k's
-// row, so there is no pivot search, and every other lane — above and below —
-// eliminates column k.  In a lane-per-row layout the rows above the pivot cost
-// no extra instructions (they were only masked off), and the solution needs no
-// back substitution: x_i = rhs_i / a_ii.  Returns false, leaving a/rhs
-// partially eliminated, as soon as a pivot is not > 0 (not numerically SPD);
-// the caller then falls back to the pivoting LU.  gj_spd_solve() of the oracle.
-template <int NMAX>
-__device__ __forceinline__ bool gj_spd_rows(double (&a)[NMAX], double& rhs, int N, int ln, double& dz) {
-  double dg = 1.0;  // this lane's pivot a_ii
-  bool ok = true;
-#pragma clang loop unroll(full)
-  for (int k = 0; k < NMAX; ++k) {
-    if (k >= N || !ok) continue;  // uniform; no `break` so the loop fully unrolls
-    const double piv = bcast(a[k], k);
-    if (!(piv > 0.0)) {
-      ok = false;
-      continue;
-    }
-    // pivot row through SGPRs (EXEC-masked readfirstlane).  The static pivot lane
-    // would allow an LDS broadcast instead (one VALU op per element less), but
-    // its store→load→fma latency chain per step measured 1.45× slower at C3.
-    // The mask is re-materialised per step (opaque): hoisted, the 32 constant
-    // masks would occupy 64 SGPRs and spill.
-    if (ln == k) dg = piv;
-    eliminate_row<NMAX>(a, rhs, k, a[k] / piv, (uint64_t)opaque64((int64_t)(1ull << k)), ln != k);
-  }
-  if (!ok) return false;
-  dz = rhs / dg;
-  return true;
-}
-
 // Dense LU with partial pivoting of the rows held in lanes [0, N) plus the
 // augmented right-hand side, then column-oriented back substitution.  On
 // success returns true and the solution entry of column `ln` in dz; returns
-// false if a pivot is exactly 0.
+// false if a pivot is exactly 0.  (A pivot-row broadcast through LDS instead of
+// SGPRs measured 24 % slower on the lone-wave lane-change LU, r02.)
 template <int NMAX>
 __device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int N, int ln, double& dz) {
   uint64_t rem = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
@@ -477,14 +444,16 @@ __device__ __forceinline__ double from_dpp_row(double v) {
 // (v_permlane*_swap reads its operands 2 wait states after a VALU write at the
 // earliest: the s_nop 1 ahead of each swap in the asm blocks.)
 //
-// NT = 2: both row halves' multipliers with ONE division.  v0 / v1 = the pivot
+// NT = 2: both row halves' negated multipliers with ONE multiplication by the
+// pivot's reciprocal rp (computed from the pivot alone, so its division runs
+// beside the column distribution instead of after it).  v0 / v1 = the pivot
 // column entries of half 0 / 1, valid in DPP row Q.  permlane32_swap puts half
 // 0's values in the lower and half 1's in the upper 32 lanes (same DPP-row
 // offset), permlane16_swap then spreads DPP row Q within each half, so lane l
-// holds w = a_{16·(l≥32) + lc, k}; one division gives t = w / piv, and a final
+// holds w = a_{16·(l≥32) + lc, k}; one product gives t = −w · rp, and a final
 // permlane32_swap hands every lane both t's (lower → half 0, upper → half 1).
 template <int Q, bool FIRST>
-__device__ __forceinline__ void col_quot_nt2(double v0, double v1, double piv, double& q0, double& q1) {
+__device__ __forceinline__ void col_quot_nt2(double v0, double v1, double rp, double& q0, double& q1) {
   const unsigned a0 = (unsigned)__double2loint(v0), a1 = (unsigned)__double2hiint(v0);
   const unsigned b0 = (unsigned)__double2loint(v1), b1 = (unsigned)__double2hiint(v1);
   unsigned x0, y0, z0, x1, y1, z1;  // per dword (0 = low, 1 = high)
@@ -508,7 +477,7 @@ __device__ __forceinline__ void col_quot_nt2(double v0, double v1, double piv, d
 #undef MCPX_NT2_ASM
   const unsigned w0 = (Q & 1) ? z0 : ((Q < 2) ? x0 : y0);
   const unsigned w1 = (Q & 1) ? z1 : ((Q < 2) ? x1 : y1);
-  const double t = __hiloint2double((int)w1, (int)w0) / piv;
+  const double t = (-__hiloint2double((int)w1, (int)w0)) * rp;  // −l = (−w)·(1/piv), exact negation
   const unsigned tl = (unsigned)__double2loint(t), thi = (unsigned)__double2hiint(t);
   const auto pl = __builtin_amdgcn_permlane32_swap(tl, tl, false, false);
   const auto ph = __builtin_amdgcn_permlane32_swap(thi, thi, false, false);
@@ -518,14 +487,20 @@ __device__ __forceinline__ void col_quot_nt2(double v0, double v1, double piv, d
 
 // acc ← fma(nl, u, acc), u = lane (16·row + R)'s `src` (DPP row_newbcast:R).
 // The DPP source is the pivot row, last written one step earlier: the column
-// distribution and the division lie between (≥ 2 wait states).
-#define MCPX_FMAC_NB(R)                                                                      \
-  case R:                                                                                    \
-    asm volatile(MCPX_DPP_PAD "v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"  \
-                 : "+v"(acc) : "v"(src), "v"(nl));                                           \
+// distribution and the multiplication lie between (≥ 2 wait states) unless the
+// compiler copies it right before the asm (PAD: s_nop 1 first).
+#define MCPX_FMAC_NB(R)                                                                                     \
+  case R:                                                                                                   \
+    if (pad)                                                                                                \
+      asm volatile("s_nop 1\n v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"    \
+                   : "+v"(acc) : "v"(src), "v"(nl));                                                        \
+    else                                                                                                    \
+      asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"               \
+                   : "+v"(acc) : "v"(src), "v"(nl));                                                        \
     break;
-template <int R>
+template <int R, bool PAD>
 __device__ __forceinline__ void fmac_row_bcast(double& acc, double src, double nl) {
+  const bool pad = PAD || MCPX_DPP_PAD_ON;
   switch (R) {
     MCPX_FMAC_NB(0) MCPX_FMAC_NB(1) MCPX_FMAC_NB(2) MCPX_FMAC_NB(3) MCPX_FMAC_NB(4) MCPX_FMAC_NB(5)
     MCPX_FMAC_NB(6) MCPX_FMAC_NB(7) MCPX_FMAC_NB(8) MCPX_FMAC_NB(9) MCPX_FMAC_NB(10) MCPX_FMAC_NB(11)
@@ -536,13 +511,18 @@ __device__ __forceinline__ void fmac_row_bcast(double& acc, double src, double n
 
 // Same with the destination as its own DPP source (the pivot half; a DPP read
 // happens before the write, so every lane sees the pivot lane's old value).
-#define MCPX_FMAC_NB_SELF(R)                                                                 \
-  case R:                                                                                    \
-    asm volatile(MCPX_DPP_PAD "v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"  \
-                 : "+v"(acc) : "v"(nl));                                                     \
+#define MCPX_FMAC_NB_SELF(R)                                                                                \
+  case R:                                                                                                   \
+    if (pad)                                                                                                \
+      asm volatile("s_nop 1\n v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"    \
+                   : "+v"(acc) : "v"(nl));                                                                  \
+    else                                                                                                    \
+      asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"               \
+                   : "+v"(acc) : "v"(nl));                                                                  \
     break;
-template <int R>
+template <int R, bool PAD>
 __device__ __forceinline__ void fmac_row_bcast_self(double& acc, double nl) {
+  const bool pad = PAD || MCPX_DPP_PAD_ON;
   switch (R) {
     MCPX_FMAC_NB_SELF(0) MCPX_FMAC_NB_SELF(1) MCPX_FMAC_NB_SELF(2) MCPX_FMAC_NB_SELF(3) MCPX_FMAC_NB_SELF(4)
     MCPX_FMAC_NB_SELF(5) MCPX_FMAC_NB_SELF(6) MCPX_FMAC_NB_SELF(7) MCPX_FMAC_NB_SELF(8) MCPX_FMAC_NB_SELF(9)
@@ -612,43 +592,44 @@ __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, 
 }
 
 // Pivot-free Gauss-Jordan of [S | rh] in the 2-D layout; gj_spd_solve() of the
-// oracle step for step (pivot k = row k; rows ≠ k: l = a_ik / a_kk,
+// oracle step for step (pivot k = row k; rows ≠ k: l = a_ik · (1 / a_kk),
 // a_ij ← fma(−l, a_kj, a_ij) for j > k, rh_i ← fma(−l, rh_k, rh_i); then the
 // pivot row a_kj ← fma(a_kj, +0, a_kj), rh_k likewise; x_i = rh_i / a_ii).  Entries of columns ≤ k are also touched in a lane
 // whose local column block straddles k; those are never read again.
 // rh[J] / x[J]: row 16J + lc, replicated over the four DPP rows.
-template <int NT>
+template <int NT, bool PAD>
 __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[NT], int N, int ln, double (&x)[NT]) {
   const int lc = ln & 15;
   double dg[NT];
 #pragma unroll
   for (int J = 0; J < NT; ++J) dg[J] = 1.0;
-  bool ok = true;
+  // A pivot that is not > 0 (not numerically SPD, or NaN) is only recorded: the
+  // remaining steps run on (discarded) values instead of branching on every pivot,
+  // which keeps the compare off the step's dependency chain.
+  bool bad = false;
 #pragma clang loop unroll(full)
   for (int k = 0; k < 16 * NT; ++k) {
-    if (k >= N || !ok) continue;
+    if (k >= N) continue;
     const int Jk = k >> 4, Rk = k & 15;        // pivot row 16·Jk + Rk
     const int Qk = k & 3, Ck = k >> 2;         // pivot column: DPP row Qk, local column Ck
     const int Ik = Ck >> 2, rk = Ck & 3;       // local column Ck = accumulator tile Ik, element rk
     const double piv = bcast(acc[Ik][Jk][rk], 16 * Qk + Rk);
-    if (!(piv > 0.0)) {
-      ok = false;
-      continue;
-    }
+    bad |= !(piv > 0.0);
+    const double rp = 1.0 / piv;  // oracle gj_spd_solve: l_i = a_ik · (1 / a_kk)
     const bool prow = lc == Rk;  // this lane holds the pivot row in half Jk
     if (prow) dg[Jk] = piv;
     double nl[NT];
     if constexpr (NT == 2) {
-      double q0, q1;
+      double q0, q1;  // −l of rows lc and 16 + lc: the fma takes −l · u exactly as fma(−l, u, a)
       switch (Qk + (k == 0 ? 4 : 0)) {  // static after unrolling
-        case 0: col_quot_nt2<0, false>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
-        case 1: col_quot_nt2<1, false>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
-        case 2: col_quot_nt2<2, false>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
-        case 3: col_quot_nt2<3, false>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
-        default: col_quot_nt2<0, true>(acc[Ik][0][rk], acc[Ik][1][rk], piv, q0, q1); break;
+        case 0: col_quot_nt2<0, false>(acc[Ik][0][rk], acc[Ik][1][rk], rp, q0, q1); break;
+        case 1: col_quot_nt2<1, false>(acc[Ik][0][rk], acc[Ik][1][rk], rp, q0, q1); break;
+        case 2: col_quot_nt2<2, false>(acc[Ik][0][rk], acc[Ik][1][rk], rp, q0, q1); break;
+        case 3: col_quot_nt2<3, false>(acc[Ik][0][rk], acc[Ik][1][rk], rp, q0, q1); break;
+        default: col_quot_nt2<0, true>(acc[Ik][0][rk], acc[Ik][1][rk], rp, q0, q1); break;
       }
-      nl[0] = -q0;  // −l: the fma takes −l · u exactly as fma(−l, u, a)
-      nl[1] = -q1;
+      nl[0] = q0;
+      nl[1] = q1;
     } else {
 #pragma unroll
       for (int J = 0; J < NT; ++J) {
@@ -661,7 +642,7 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
           case 3: colv = from_dpp_row<3, false>(acc[Ik][J][rk]); break;
           default: colv = from_dpp_row<0, true>(acc[Ik][J][rk]); break;  // k = 0: DPP row 0
         }
-        nl[J] = -(colv / piv);
+        nl[J] = (-colv) * rp;
       }
     }
     // The pivot row takes the same fma with multiplier +0 (a_kj ← fma(a_kj, +0, a_kj),
@@ -675,7 +656,7 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
       for (int c = 0; c < 4 * NT; ++c) {
         if (4 * c + 3 <= k) continue;  // every column of this local block ≤ k
         switch (Rk) {
-#define MCPX_CASE(R) case R: fmac_row_bcast<R>(acc[c >> 2][J][c & 3], acc[c >> 2][Jk][c & 3], nl[J]); break;
+#define MCPX_CASE(R) case R: fmac_row_bcast<R, PAD>(acc[c >> 2][J][c & 3], acc[c >> 2][Jk][c & 3], nl[J]); break;
           MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
           MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14)
           MCPX_CASE(15)
@@ -683,7 +664,7 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
         }
       }
       switch (Rk) {
-#define MCPX_CASE(R) case R: fmac_row_bcast<R>(rh[J], rh[Jk], nl[J]); break;
+#define MCPX_CASE(R) case R: fmac_row_bcast<R, PAD>(rh[J], rh[Jk], nl[J]); break;
         MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
         MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14) MCPX_CASE(15)
 #undef MCPX_CASE
@@ -694,7 +675,7 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
       for (int c = 0; c < 4 * NT; ++c) {
         if (4 * c + 3 <= k) continue;
         switch (Rk) {
-#define MCPX_CASE(R) case R: fmac_row_bcast_self<R>(acc[c >> 2][Jk][c & 3], nl[Jk]); break;
+#define MCPX_CASE(R) case R: fmac_row_bcast_self<R, PAD>(acc[c >> 2][Jk][c & 3], nl[Jk]); break;
           MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
           MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14)
           MCPX_CASE(15)
@@ -702,14 +683,14 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
         }
       }
       switch (Rk) {
-#define MCPX_CASE(R) case R: fmac_row_bcast_self<R>(rh[Jk], nl[Jk]); break;
+#define MCPX_CASE(R) case R: fmac_row_bcast_self<R, PAD>(rh[Jk], nl[Jk]); break;
         MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
         MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14) MCPX_CASE(15)
 #undef MCPX_CASE
       }
     }
   }
-  if (!ok) return false;
+  if (bad) return false;
 #pragma unroll
   for (int J = 0; J < NT; ++J) x[J] = rh[J] / dg[J];
   return true;
@@ -893,7 +874,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
           double rh2[NT], x2[NT];
 #pragma unroll
           for (int J = 0; J < NT; ++J) rh2[J] = (16 * J + (ln & 15) < n) ? sB[16 * J + (ln & 15)] : 0.0;
-          ok = gj2d_spd<NT>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, x2);
+          ok = gj2d_spd<NT, (NC == 0)>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, x2);
 #pragma unroll
           for (int J = 0; J < NT; ++J)
             if ((ln >> 4) == J) dz = x2[J];  // lane 16J + lc owns row 16J + lc

@@ -93,6 +93,10 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   int status = 0;                     // :69
   int outer = 1;                      // :70
   int newton = 0;
+#if MCPX_STAMPS
+  uint64_t st_acc[4] = {0, 0, 0, 0};
+  uint64_t st_last = __builtin_amdgcn_s_memtime();
+#endif
   while (kkt > tol && eps > tol && outer < args.max_outer) {  // :71
     int inner = 1;                                             // :72
     status = 0;                                                // :73
@@ -117,6 +121,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
       // ‖F‖∞ with NaN propagation (:107), taken now, committed after the step
       const double kkt_step = ballot(aF != aF) ? __builtin_nan("") : wave_max_nonneg(aF);
       __syncthreads();
+      MCPX_STAMP(0);
 
       // ---- Newton system (∇F + tol·I) δz = −F (:81-90) ----------------------
       double dz = 0.0;
@@ -139,13 +144,14 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
         }
         __syncthreads();
         // row i of S = (P + tol·I) − Q D⁻¹ R and rr_i = −F_Gi − Σ_k Q_ik ty_k, k ascending
+        // lanes ≥ n hold a copy of row 0: never a pivot row, never updated (lu_solve_rows)
         const int i = lx ? lane : 0;
+        const double dg = blk[OFF_P + i * n + i] + tol;  // the diagonal entry, one add
         double a[NMAX];
 #pragma unroll
         for (int j = 0; j < NMAX; ++j) {
-          double v = (j < n) ? blk[OFF_P + j * n + i] : 0.0;
-          if (j == lane) v += tol;
-          a[j] = lx ? v : 0.0;
+          const double v = (j < n) ? blk[OFF_P + j * n + i] : 0.0;
+          a[j] = (j == lane) ? dg : v;
         }
         double rhs = lx ? -Fs[i] : 0.0;
         // only Q's structural nonzeros of row i, K(i) ascending (mcpx_nl_qk_*, generated);
@@ -158,7 +164,9 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
           for (int j = 0; j < n; ++j) a[j] = fma(q, RDt[k * n + j], a[j]);
           rhs = fma(q, sTy[k], rhs);
         }
+        MCPX_STAMP(1);
         ok = lu_solve_rows<NMAX>(a, rhs, opaque(n), lane, dz);
+        MCPX_STAMP(2);
         if (ok) {
           if (lx) dzs[lane] = dz;
           __syncthreads();
@@ -305,6 +313,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
         }
       }
       kkt = kkt_step;  // :107
+      MCPX_STAMP(3);
       ++inner;         // :108
       ++newton;
     }
@@ -330,6 +339,10 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
     const uint64_t bits = ballot(act);
     if (lane == 0) args.active_mask[inst] = bits;
   }
+#if MCPX_STAMPS
+  if (lane == 0 && args.stamps)
+    for (int i = 0; i < 4; ++i) args.stamps[inst * 4 + i] = st_acc[i];
+#endif
   if (lane == 0) {
     args.kkt_error[inst] = kkt;
     args.eps[inst] = eps;

@@ -45,7 +45,7 @@
  *    every pivot of elimination without pivoting is > 0 — positive definite,
  *    so it is solved by pivot-free Gauss-Jordan elimination (gj_spd_solve:
  *    pivot k is row k; every other row i, above and below, is updated with
- *    l_i = a_ik / a_kk, a_ij ← fma(−l_i, a_kj, a_ij) for j > k and the rhs,
+ *    l_i = a_ik · r_k with r_k = 1 / a_kk, a_ij ← fma(−l_i, a_kj, a_ij) for j > k and the rhs,
  *    then the pivot row itself a_kj ← fma(a_kj, +0, a_kj) (identity unless
  *    non-finite; the GPU updates every lane uniformly); x_i = b_i / a_ii).  If M is not symmetric or a pivot is not
  *    > 0 (indefinite / NaN), that Newton step falls back to the partial-
@@ -264,11 +264,12 @@ static int gj_spd_solve(int n, double* S /* n×n row-major, destroyed */, double
   for (int k = 0; k < n; ++k) {
     const double piv = S[(size_t)k * n + k];
     if (!(piv > 0.0)) return 1;
+    const double rp = 1.0 / piv; /* one reciprocal per pivot, off the GPU's multiplier chain */
     const double* u = S + (size_t)k * n;
     for (int i = 0; i < n; ++i) {
       if (i == k) continue;
       double* a = S + (size_t)i * n;
-      const double l = a[k] / piv;
+      const double l = a[k] * rp;
       for (int j = k + 1; j < n; ++j) a[j] = fma(-l, u[j], a[j]);
       b[i] = fma(-l, b[k], b[i]);
     }

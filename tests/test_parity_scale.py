@@ -58,7 +58,7 @@ def test_schur_equals_full_lu_on_bench_inputs(oracle_lib, n, m, B):
 def test_sparse_stress_set_divergences_are_recorded(oracle_lib):
     """0.9-sparse QPs (the reference benchmark's default sparsity), 512 instances:
     only 10 are :solved under either solver.  The two exact eliminations differ in
-    rounding, which moves some failing trajectories: 9 Newton counts, 10 α traces
+    rounding, which moves some failing trajectories: 12 Newton counts, 12 α traces
     and 1 final active set differ — never a status, never a solved instance."""
     th = generate_global_slice(1, 16, 8, 0.9, 0, 512)
     r = _solve_both(oracle_lib, 16, 8, th)
@@ -68,7 +68,7 @@ def test_sparse_stress_set_divergences_are_recorded(oracle_lib):
     newton = a["newton_iters"] != d["newton_iters"]
     alpha = (a["alpha_trace"] != d["alpha_trace"]).any(axis=(1, 2))
     active = (a["active_mask"] != d["active_mask"]).any(axis=1)
-    assert (int(newton.sum()), int(alpha.sum()), int(active.sum())) == (9, 10, 1)
+    assert (int(newton.sum()), int(alpha.sum()), int(active.sum())) == (12, 12, 1)
     diverged = newton | alpha | active | (a["outer_iters"] != d["outer_iters"])
     assert np.all(a["status"][diverged] == 1)
     ok = a["status"] == 0

@@ -98,8 +98,12 @@ def wait_state_hazards(insts, want: str):
             if kk != k:
                 break
             if ll:
-                j -= 1
-                continue
+                # a join point: another predecessor (a branch to this label) may have
+                # written the source just before jumping; only the fall-through path
+                # is walked, so a reader this close to a label is reported unless it
+                # is padded on its own
+                bad.append(f"WAIT-STATE HAZARD (join point {tt}) in {k}:\n   {t}  ({states} wait states after the label)")
+                break
             o = tt.split()[0]
             if o == "s_nop":
                 states += int(tt.split()[1], 0) + 1

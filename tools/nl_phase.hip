@@ -1,0 +1,71 @@
+// Diagnostic: per-phase s_memtime cycles of a generated nonlinear module's one-wave kernel
+// (module built with -DMCPX_STAMPS=1; see tools/nl_phase.py, which writes θ and runs this).
+//   nl_phase <module.hsaco> <kernel> <theta.bin> n m p B
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../mcp_amd/csrc/ipm_kernel.h"
+
+int main(int argc, char** argv) {
+  if (argc < 8) { fprintf(stderr, "usage\n"); return 2; }
+  const char *mod = argv[1], *kname = argv[2], *thf = argv[3];
+  const int n = atoi(argv[4]), m = atoi(argv[5]), p = atoi(argv[6]), B = atoi(argv[7]);
+  std::vector<double> th((size_t)B * p);
+  FILE* f = fopen(thf, "rb");
+  if (!f || fread(th.data(), 8, th.size(), f) != th.size()) { fprintf(stderr, "theta read failed\n"); return 2; }
+  fclose(f);
+  hipModule_t M;
+  hipFunction_t K;
+  if (hipModuleLoad(&M, mod) != hipSuccess || hipModuleGetFunction(&K, M, kname) != hipSuccess) {
+    fprintf(stderr, "module/kernel load failed\n");
+    return 2;
+  }
+  double *dth, *x, *y, *s, *kkt, *eps;
+  int *outer, *status, *newton;
+  uint64_t* stamps;
+  (void)hipMalloc(&dth, th.size() * 8);
+  (void)hipMemcpy(dth, th.data(), th.size() * 8, hipMemcpyHostToDevice);
+  (void)hipMalloc(&x, (size_t)B * n * 8); (void)hipMalloc(&y, (size_t)B * m * 8); (void)hipMalloc(&s, (size_t)B * m * 8);
+  (void)hipMalloc(&kkt, B * 8); (void)hipMalloc(&eps, B * 8);
+  (void)hipMalloc(&outer, B * 4); (void)hipMalloc(&status, B * 4); (void)hipMalloc(&newton, B * 4);
+  (void)hipMalloc(&stamps, (size_t)B * 4 * 8);
+  mcpx::KernelArgs a{};
+  a.theta = dth; a.theta_ld = p; a.x = x; a.y = y; a.s = s; a.kkt_error = kkt; a.eps = eps;
+  a.outer_iters = outer; a.status = status; a.newton_iters = newton; a.stamps = stamps;
+  a.n = n; a.m = m; a.family = MCPX_FAMILY_NONLINEAR; a.solver = MCPX_LINSOLVE_SCHUR;
+  a.max_inner = 20; a.max_outer = 50; a.n_trials = 15; a.tol = 1e-6; a.decay = 0.5; a.c_tau = 1.0 - 0.995;
+  for (int k = 0; k <= a.max_inner; ++k) { a.tight[k] = 1 - exp(-0.1 * k); a.loose[k] = 1 + exp(-0.5 * k); }
+  size_t sz = sizeof a;
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  float ms = 0;
+  for (int rep = 0; rep < 2; ++rep) {
+    (void)hipEventRecord(e0, 0);
+    if (hipModuleLaunchKernel(K, B, 1, 1, 64, 1, 1, 0, 0, nullptr, cfg) != hipSuccess) { fprintf(stderr, "launch failed\n"); return 2; }
+    (void)hipEventRecord(e1, 0);
+    (void)hipDeviceSynchronize();
+    (void)hipEventElapsedTime(&ms, e0, e1);
+  }
+  std::vector<uint64_t> st((size_t)B * 4);
+  std::vector<int> nw(B), stt(B);
+  (void)hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(nw.data(), newton, B * 4, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(stt.data(), status, B * 4, hipMemcpyDeviceToHost);
+  const char* nm[] = {"eval+F+kkt", "schur prep+form", "LU", "dy/ds+linesearch+update"};
+  for (int grp = 0; grp < 2; ++grp) {  // solved, failed
+    double tot[4] = {0, 0, 0, 0}, steps = 0; int cnt = 0, mx = 0;
+    for (int b = 0; b < B; ++b) {
+      if ((stt[b] != 0) != (grp == 1)) continue;
+      for (int i = 0; i < 4; ++i) tot[i] += st[(size_t)b * 4 + i];
+      steps += nw[b]; ++cnt; mx = nw[b] > mx ? nw[b] : mx;
+    }
+    const double all = tot[0] + tot[1] + tot[2] + tot[3];
+    printf("[%s] B=%d kernel %.3f ms  %s: %d instances, newton mean %.1f max %d, cycles per Newton step %.0f\n", kname,
+           B, ms, grp ? "failed" : "solved", cnt, cnt ? steps / cnt : 0.0, mx, steps ? all / steps : 0.0);
+    for (int i = 0; i < 4; ++i) printf("  %-26s %5.1f%%  %8.0f cyc/step\n", nm[i], all ? 100 * tot[i] / all : 0.0, steps ? tot[i] / steps : 0.0);
+  }
+  return 0;
+}
