@@ -51,9 +51,25 @@ class Module:
             self.handle = None
 
 
+def alloc_host_outputs(B: int, n: int, m: int, trace_len: int = 0) -> dict:
+    """Host result buffers of solve_batch(out=...), first-touched here: reused across
+    calls they spare the D→H copy the page faults of fresh numpy pages."""
+    words = max(1, (m + 63) // 64)
+    r = dict(
+        x=np.zeros((B, n)), y=np.zeros((B, m)), s=np.zeros((B, m)), kkt_error=np.zeros(B),
+        eps=np.zeros(B), outer_iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32),
+        newton_iters=np.zeros(B, np.int32),
+        active_mask=np.zeros((B, words), np.uint64) if m <= 64 else None,
+        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+    )
+    return r
+
+
 def solve_batch(family: int, n: int, m: int, theta, *, x0=None, y0=None, s0=None, params=None,
-                num_devices: int = 0, trace_len: int = 0, module: Module | None = None, **kw) -> dict:
-    """Solve B instances on the GPU(s).  theta: (B, ≥p) float64 host array."""
+                num_devices: int = 0, trace_len: int = 0, module: Module | None = None, out: dict | None = None,
+                **kw) -> dict:
+    """Solve B instances on the GPU(s).  theta: (B, ≥p) float64 host array.  `out`: result
+    buffers from alloc_host_outputs (filled in place and returned), else fresh arrays."""
     theta = np.ascontiguousarray(theta, dtype=np.float64)
     if theta.ndim == 1:
         theta = theta[None, :]
@@ -62,13 +78,19 @@ def solve_batch(family: int, n: int, m: int, theta, *, x0=None, y0=None, s0=None
     conv = lambda a, k: None if a is None else np.ascontiguousarray(np.broadcast_to(a, (B, k)), dtype=np.float64)
     x0, y0, s0 = conv(x0, n), conv(y0, m), conv(s0, m)
     words = max(1, (m + 63) // 64)
-    r = dict(
-        x=np.empty((B, n)), y=np.empty((B, m)), s=np.empty((B, m)), kkt_error=np.empty(B),
-        eps=np.empty(B), outer_iters=np.empty(B, np.int32), status=np.empty(B, np.int32),
-        newton_iters=np.empty(B, np.int32),
-        active_mask=np.empty((B, words), np.uint64) if m <= 64 else None,
-        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
-    )
+    if out is not None:
+        r = out
+        if r["x"].shape != (B, n) or r["y"].shape != (B, m) or r["status"].shape != (B,) or (
+                trace_len > 0 and r["alpha_trace"].shape[1] < trace_len):
+            raise ValueError("out buffers do not match the batch (alloc_host_outputs(B, n, m, trace_len))")
+    else:
+        r = dict(
+            x=np.empty((B, n)), y=np.empty((B, m)), s=np.empty((B, m)), kkt_error=np.empty(B),
+            eps=np.empty(B), outer_iters=np.empty(B, np.int32), status=np.empty(B, np.int32),
+            newton_iters=np.empty(B, np.int32),
+            active_mask=np.empty((B, words), np.uint64) if m <= 64 else None,
+            alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+        )
     out = _abi.Out(_ptr(r["x"]), _ptr(r["y"]), _ptr(r["s"]), _ptr(r["kkt_error"]), _ptr(r["eps"]),
                    _ptr(r["outer_iters"]), _ptr(r["status"]), _ptr(r["newton_iters"]),
                    _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,

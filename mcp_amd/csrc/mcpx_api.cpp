@@ -369,32 +369,81 @@ struct AsyncBuf {  // stream-ordered device buffer, freed on the stream it was a
   ~AsyncBuf() { if (p) (void)hipFreeAsync(p, st); }
 };
 
-constexpr int kMaxHostStreams = 8;
-
-// Streams of the host-buffer pipeline: MCPX_HOST_STREAMS (A/B knob, 1..8, default 2).
-int host_streams() {
-  const char* e = std::getenv("MCPX_HOST_STREAMS");
-  const int v = e ? std::atoi(e) : 2;
-  return v < 1 ? 1 : (v > kMaxHostStreams ? kMaxHostStreams : v);
+// θ buffers the host-buffer pipeline rotates through: MCPX_HOST_BUFFERS (A/B knob, 2..8,
+// default 3: chunk c+1 and c+2 upload while chunk c solves).
+constexpr int kMaxHostBufs = 8;
+int host_buffers() {
+  const char* e = std::getenv("MCPX_HOST_BUFFERS");
+  const int v = e ? std::atoi(e) : 3;
+  return v < 2 ? 2 : (v > kMaxHostBufs ? kMaxHostBufs : v);
 }
 
-struct Streams {
-  hipStream_t s[kMaxHostStreams] = {};
-  ~Streams() {
-    for (auto& x : s)
-      if (x) (void)hipStreamDestroy(x);
+// Instances per pipelined chunk: MCPX_HOST_CHUNK (A/B knob, ≥ 1024, default 4096:
+// profiles/r02/host_pipeline.jsonl).
+int64_t host_chunk() {
+  const char* e = std::getenv("MCPX_HOST_CHUNK");
+  const long long v = e ? std::atoll(e) : 4096;
+  return v < 1024 ? 1024 : v;
+}
+
+// The pipeline's two streams and per-buffer events.  Creating streams per call maps new
+// hardware queues every time (≈10 ms per call: profiles/r02/host_pipeline_trace.txt), so
+// they come from a process-wide free list per device: a call takes one Pipe and gives
+// it back when it returns, concurrent calls get different ones (the ABI stays
+// reentrant), and none is ever destroyed (no HIP calls during process teardown).
+struct Pipe {
+  hipStream_t up = nullptr, comp = nullptr;  // H→D uploads (serialised: full PCIe rate each), kernels
+  hipEvent_t copied[kMaxHostBufs] = {}, consumed[kMaxHostBufs] = {};
+  hipError_t init() {
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&comp, hipStreamNonBlocking)) != hipSuccess) return e;
+    for (int k = 0; k < kMaxHostBufs; ++k) {
+      if ((e = hipEventCreateWithFlags(&copied[k], hipEventDisableTiming)) != hipSuccess) return e;
+      if ((e = hipEventCreateWithFlags(&consumed[k], hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
 };
 
-// One device's share of mcpx_solve_batch: instances [b0, b0+nb), pipelined in
-// chunks of kChunk instances over S streams (default 2): θ (and warm starts) of
-// chunk c go up on stream c mod S while the previous chunks solve on the others;
-// the outputs land in whole-shard device buffers and come back once, after every
-// stream drained.
+std::mutex g_pipe_mu;
+std::map<int, std::vector<Pipe*>> g_pipe_free;
+
+struct PipeLease {  // a Pipe of device `dev` for the duration of one call (current device = dev)
+  Pipe* p = nullptr;
+  int dev = -1;
+  int acquire(int d) {
+    dev = d;
+    {
+      std::lock_guard<std::mutex> lock(g_pipe_mu);
+      auto& v = g_pipe_free[d];
+      if (!v.empty()) {
+        p = v.back();
+        v.pop_back();
+        return MCPX_OK;
+      }
+    }
+    Pipe* q = new Pipe;
+    if (hipError_t e = q->init(); e != hipSuccess) return fail(MCPX_EHIP, "stream setup: %s", hipGetErrorString(e));
+    p = q;
+    return MCPX_OK;
+  }
+  ~PipeLease() {
+    if (!p) return;
+    std::lock_guard<std::mutex> lock(g_pipe_mu);
+    g_pipe_free[dev].push_back(p);
+  }
+};
+
+// One device's share of mcpx_solve_batch: instances [b0, b0+nb), pipelined in chunks
+// of MCPX_HOST_CHUNK instances through NB rotating θ buffers.  θ (and warm starts) of
+// every chunk go up on ONE upload stream, back to back at the full host-link rate; the
+// compute stream runs chunk c once its upload is done (event), and the upload of chunk
+// c + NB waits for chunk c's kernel to release its buffer (event).  Outputs land in
+// whole-shard device buffers and come back once, after the last kernel.
 int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                 const double* s0, const mcpx_params* prm, mcpx_out* o, int64_t b0, int64_t nb,
                 mcpx_module* mod = nullptr) {
-  constexpr int64_t kChunk = 8192;
   HIP_TRY(hipSetDevice(dev));
   int rc = check_device(dev);
   if (rc) return rc;
@@ -405,46 +454,48 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   const int n = d->n, m = d->m;
   if (m > 64 && o->active_mask) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
   if ((rc = keep_pool_warm(dev))) return rc;
-  Streams ss;
-  const int S = host_streams();
-  for (int k = 0; k < S; ++k) HIP_TRY(hipStreamCreateWithFlags(&ss.s[k], hipStreamNonBlocking));
-  const int64_t ch = std::min(kChunk, nb);
+  PipeLease lease;
+  if ((rc = lease.acquire(dev))) return rc;
+  Pipe* P = lease.p;
+  const int NB = host_buffers();
+  const int64_t ch = std::min(host_chunk(), nb);
   const int64_t ld = d->theta_ld;
-  AsyncBuf<double> th[kMaxHostStreams], wx[kMaxHostStreams], wy[kMaxHostStreams], ws[kMaxHostStreams];
+  hipStream_t cs = P->comp, us = P->up;
+  AsyncBuf<double> th[kMaxHostBufs], wx[kMaxHostBufs], wy[kMaxHostBufs], ws[kMaxHostBufs];
   AsyncBuf<double> x, y, s, kkt, eps;
   AsyncBuf<int32_t> outer, status, newton;
   AsyncBuf<uint64_t> am;
   AsyncBuf<uint8_t> tr;
-  hipStream_t s0st = ss.s[0];
-  for (int k = 0; k < S; ++k) {
-    HIP_TRY(th[k].alloc((size_t)ch * ld, ss.s[k]));
-    if (x0) HIP_TRY(wx[k].alloc((size_t)ch * n, ss.s[k]));
-    if (y0) HIP_TRY(wy[k].alloc((size_t)ch * m, ss.s[k]));
-    if (s0) HIP_TRY(ws[k].alloc((size_t)ch * m, ss.s[k]));
+  const int nbuf = (int)std::min<int64_t>(NB, (nb + ch - 1) / std::max<int64_t>(ch, 1));
+  for (int k = 0; k < nbuf; ++k) {  // every buffer lives on the compute stream (allocated, used, freed there)
+    HIP_TRY(th[k].alloc((size_t)ch * ld, cs));
+    if (x0) HIP_TRY(wx[k].alloc((size_t)ch * n, cs));
+    if (y0) HIP_TRY(wy[k].alloc((size_t)ch * m, cs));
+    if (s0) HIP_TRY(ws[k].alloc((size_t)ch * m, cs));
   }
-  HIP_TRY(x.alloc((size_t)nb * n, s0st)); HIP_TRY(y.alloc((size_t)nb * m, s0st)); HIP_TRY(s.alloc((size_t)nb * m, s0st));
-  HIP_TRY(kkt.alloc(nb, s0st)); HIP_TRY(eps.alloc(nb, s0st)); HIP_TRY(outer.alloc(nb, s0st));
-  HIP_TRY(status.alloc(nb, s0st));
-  if (o->newton_iters) HIP_TRY(newton.alloc(nb, s0st));
-  if (o->active_mask) HIP_TRY(am.alloc(nb, s0st));
+  HIP_TRY(x.alloc((size_t)nb * n, cs)); HIP_TRY(y.alloc((size_t)nb * m, cs)); HIP_TRY(s.alloc((size_t)nb * m, cs));
+  HIP_TRY(kkt.alloc(nb, cs)); HIP_TRY(eps.alloc(nb, cs)); HIP_TRY(outer.alloc(nb, cs));
+  HIP_TRY(status.alloc(nb, cs));
+  if (o->newton_iters) HIP_TRY(newton.alloc(nb, cs));
+  if (o->active_mask) HIP_TRY(am.alloc(nb, cs));
   const bool want_tr = o->alpha_trace && o->trace_len > 0;
   if (want_tr) {
-    HIP_TRY(tr.alloc((size_t)nb * o->trace_len * 2, s0st));
-    HIP_TRY(hipMemsetAsync(tr.p, 254, (size_t)nb * o->trace_len * 2, s0st));
+    HIP_TRY(tr.alloc((size_t)nb * o->trace_len * 2, cs));
+    HIP_TRY(hipMemsetAsync(tr.p, 254, (size_t)nb * o->trace_len * 2, cs));
   }
-  hipEvent_t ready;  // the whole-shard allocations (stream 0) before the other streams use them
-  HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(ready, s0st));
-  for (int k = 1; k < S; ++k) HIP_TRY(hipStreamWaitEvent(ss.s[k], ready, 0));
-  (void)hipEventDestroy(ready);
+  // the allocations (compute stream) before the first upload into them
+  HIP_TRY(hipEventRecord(P->consumed[0], cs));
+  HIP_TRY(hipStreamWaitEvent(us, P->consumed[0], 0));
   for (int64_t c0 = 0, ci = 0; c0 < nb; c0 += ch, ++ci) {
-    const int k = (int)(ci % S);
-    hipStream_t st = ss.s[k];
+    const int k = (int)(ci % nbuf);
     const int64_t cn = std::min(ch, nb - c0), g0 = b0 + c0;
-    HIP_TRY(hipMemcpyAsync(th[k].p, theta + g0 * ld, sizeof(double) * (size_t)cn * ld, hipMemcpyHostToDevice, st));
-    if (x0) HIP_TRY(hipMemcpyAsync(wx[k].p, x0 + g0 * n, sizeof(double) * cn * n, hipMemcpyHostToDevice, st));
-    if (y0) HIP_TRY(hipMemcpyAsync(wy[k].p, y0 + g0 * m, sizeof(double) * cn * m, hipMemcpyHostToDevice, st));
-    if (s0) HIP_TRY(hipMemcpyAsync(ws[k].p, s0 + g0 * m, sizeof(double) * cn * m, hipMemcpyHostToDevice, st));
+    if (ci >= nbuf) HIP_TRY(hipStreamWaitEvent(us, P->consumed[k], 0));  // chunk ci - nbuf released buffer k
+    HIP_TRY(hipMemcpyAsync(th[k].p, theta + g0 * ld, sizeof(double) * (size_t)cn * ld, hipMemcpyHostToDevice, us));
+    if (x0) HIP_TRY(hipMemcpyAsync(wx[k].p, x0 + g0 * n, sizeof(double) * cn * n, hipMemcpyHostToDevice, us));
+    if (y0) HIP_TRY(hipMemcpyAsync(wy[k].p, y0 + g0 * m, sizeof(double) * cn * m, hipMemcpyHostToDevice, us));
+    if (s0) HIP_TRY(hipMemcpyAsync(ws[k].p, s0 + g0 * m, sizeof(double) * cn * m, hipMemcpyHostToDevice, us));
+    HIP_TRY(hipEventRecord(P->copied[k], us));
+    HIP_TRY(hipStreamWaitEvent(cs, P->copied[k], 0));
     mcpx_out od{};
     od.x = x.p + c0 * n; od.y = y.p + c0 * m; od.s = s.p + c0 * m; od.kkt_error = kkt.p + c0; od.eps = eps.p + c0;
     od.outer_iters = outer.p + c0; od.status = status.p + c0; od.newton_iters = newton.p ? newton.p + c0 : nullptr;
@@ -453,9 +504,14 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
     od.trace_len = want_tr ? o->trace_len : 0;
     mcpx_desc dd = *d;
     dd.batch = cn;
-    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, st, mod, wg))) return rc;
+    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, cs, mod, wg))) {
+      (void)hipStreamSynchronize(us);  // no upload may still target a buffer freed on return
+      return rc;
+    }
+    HIP_TRY(hipEventRecord(P->consumed[k], cs));
   }
-  for (int k = 0; k < S; ++k) HIP_TRY(hipStreamSynchronize(ss.s[k]));
+  HIP_TRY(hipStreamSynchronize(us));
+  HIP_TRY(hipStreamSynchronize(cs));
   auto back = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
     return bytes ? hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) : hipSuccess;
   };
