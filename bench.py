@@ -375,7 +375,10 @@ def main_lane_change(a, world, rank, local, dist, pl):
                                                                   [newton, solved])
     if rank != 0:
         return
-    cfg = {"mode": "c4", "horizon": a.lane_change, "batch_per_gpu": B, "linear_solver": ls}
+    # the generated module's content hash (its kernel headers included) keys the evidence too:
+    # the nonlinear kernels live in the module, not in libmcpx.so
+    cfg = {"mode": "c4", "horizon": a.lane_change, "batch_per_gpu": B, "linear_solver": ls,
+           "module": mcp.nl.module_key()}
     key = f"c4_lane_t{a.lane_change}_b{B}"
     ev = evidence(key, cfg)
     kernel = "mcpx_nl_solve_" + ls + ("" if mcp.nl.solvers()[ls] else "_wg")

@@ -874,7 +874,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
           double rh2[NT], x2[NT];
 #pragma unroll
           for (int J = 0; J < NT; ++J) rh2[J] = (16 * J + (ln & 15) < n) ? sB[16 * J + (ln & 15)] : 0.0;
-          ok = gj2d_spd<NT, (NC == 0)>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, x2);
+          ok = gj2d_spd<NT, (NC == 0)>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, x2);  // opaque: with a constant
+          // dimension the scheduler merges the 32 steps (+5 % VALU in the fast pass)
 #pragma unroll
           for (int J = 0; J < NT; ++J)
             if ((ln >> 4) == J) dz = x2[J];  // lane 16J + lc owns row 16J + lc

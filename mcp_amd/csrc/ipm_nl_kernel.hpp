@@ -21,7 +21,7 @@
 // lane ↔ row map:
 //   SCHUR   (∂H/∂y ≡ 0) δs, then δy eliminated exactly; lane i < n owns row i
 //           of S = (P + tol·I) − Q D⁻¹ R, D = tol + s/(y + tol)  (n ≤ 64, m ≤ 128),
-//           formed from Q's structural nonzeros only (oracle: the same terms);
+//           formed from Q's and R's structural nonzeros only (oracle: the same terms);
 //   REDUCED δs eliminated; lanes [0, n+m) own the (n+m)-dim system;
 //   DENSE   lanes [0, n+2m) own the rows of ∇F + tol·I;
 // all three factor with the register LU with partial pivoting of the QP /
@@ -65,7 +65,8 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   constexpr int NZ = imax(1, N), MZ = imax(1, m);
   __shared__ double blk[BLK];
   __shared__ double zs[NZ], dzs[NZ], Fs[NZ];
-  __shared__ double RDt[SCH ? imax(1, m * n) : 1];  // SCHUR: R_kj·D_k⁻¹ at k·n + j
+  constexpr int LDR = n + 1;  // SCHUR: lane-private LDS rows of S (odd stride: 2-way bank conflicts at most)
+  __shared__ double Srow[SCH ? imax(1, n * LDR) : 1];
   __shared__ double sRw[SCH ? MZ : 1], sDi[SCH ? MZ : 1], sRy[SCH ? MZ : 1], sTy[SCH ? MZ : 1];
 
   const int lane = threadIdx.x;
@@ -139,7 +140,6 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
             sDi[k] = Di;
             sRy[k] = ry;
             sTy[k] = ry * Di;
-            for (int j = 0; j < n; ++j) RDt[k * n + j] = blk[OFF_R + j * m + k] * Di;
           }
         }
         __syncthreads();
@@ -154,15 +154,26 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
           a[j] = (j == lane) ? dg : v;
         }
         double rhs = lx ? -Fs[i] : 0.0;
-        // only Q's structural nonzeros of row i, K(i) ascending (mcpx_nl_qk_*, generated);
-        // lanes loop over their own list (at most 3 terms in the lane-change game, against m)
+        // − Q D⁻¹ R over the structural nonzeros only (mcpx_nl_qk_* / mcpx_nl_rj_*, generated):
+        // entry (i, j) takes fma(−Q_ik, R_kj·D_k⁻¹, ·) for k ∈ K(i) with j ∈ J(k), k ascending
+        // (the oracle's chain; at most 3 × 4 terms a row in the lane-change game).  The row
+        // indices are per lane, so the row goes through its lane's own LDS row and back.
         const int t0 = lx ? mcpx_nl_qk_ptr[i] : 0, t1 = lx ? mcpx_nl_qk_ptr[i + 1] : 0;
-        for (int t = t0; t < t1; ++t) {
-          const int k = mcpx_nl_qk_idx[t];
-          const double q = -blk[OFF_Q + k * n + i];
+        if (t1 > t0) {
+          double* row = Srow + i * LDR;
 #pragma unroll
-          for (int j = 0; j < n; ++j) a[j] = fma(q, RDt[k * n + j], a[j]);
-          rhs = fma(q, sTy[k], rhs);
+          for (int j = 0; j < n; ++j) row[j] = a[j];
+          for (int t = t0; t < t1; ++t) {
+            const int k = mcpx_nl_qk_idx[t];
+            const double q = -blk[OFF_Q + k * n + i], Di = sDi[k];
+            for (int u = mcpx_nl_rj_ptr[k]; u < mcpx_nl_rj_ptr[k + 1]; ++u) {
+              const int j = mcpx_nl_rj_idx[u];
+              row[j] = fma(q, blk[OFF_R + j * m + k] * Di, row[j]);
+            }
+            rhs = fma(q, sTy[k], rhs);
+          }
+#pragma unroll
+          for (int j = 0; j < n; ++j) a[j] = row[j];
         }
         MCPX_STAMP(1);
         ok = lu_solve_rows<NMAX>(a, rhs, opaque(n), lane, dz);
@@ -359,7 +370,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
 #define MCPX_NL_CAN_DENSE (MCPX_NL_N + 2 * MCPX_NL_M >= 1 && MCPX_NL_N + 2 * MCPX_NL_M <= 64)
 #define MCPX_NL_SCHUR_LDS                                                                             \
   (8 * (MCPX_NL_N * MCPX_NL_N + 2 * MCPX_NL_N * MCPX_NL_M + MCPX_NL_N + MCPX_NL_M +                   \
-        MCPX_NL_M * MCPX_NL_N + 3 * (MCPX_NL_N + 2 * MCPX_NL_M) + 4 * MCPX_NL_M))
+        MCPX_NL_N * (MCPX_NL_N + 1) + 3 * (MCPX_NL_N + 2 * MCPX_NL_M) + 4 * MCPX_NL_M))
 #define MCPX_NL_CAN_SCHUR                                                                             \
   (!MCPX_NL_HAS_S && MCPX_NL_N >= 1 && MCPX_NL_N <= 64 && MCPX_NL_M <= 128 &&                         \
    MCPX_NL_SCHUR_LDS <= 160 * 1024 - 2048)

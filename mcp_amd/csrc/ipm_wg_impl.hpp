@@ -554,17 +554,22 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
           for (int k = wave; k < m; k += NWAVE)  // R_kj · D_k⁻¹, row k (wave per row, lanes over j)
             for (int j = lane; j < n; j += 64) RD[k * n + j] = blk[GEN::OFF_R + j * m + k] * sD[k];
           __syncthreads();
-          // S = (P + tol·I) + Σ_{k ∈ K(i)} (−Q_ik)(R_kj D_k⁻¹), k ascending over Q's structural
-          // nonzeros of row i (the oracle's terms), and rr_i = −F_Gi + Σ_{k ∈ K(i)} (−Q_ik) ty_k
+          // S = (P + tol·I) + Σ (−Q_ik)(R_kj D_k⁻¹) over k ∈ K(i) (Q's structural nonzeros of
+          // row i) with j ∈ J(k) (R's of row k), k ascending (the oracle's terms), and
+          // rr_i = −F_Gi + Σ_{k ∈ K(i)} (−Q_ik) ty_k
           const int32_t* qp = GEN::qk_ptr();
           const int32_t* qi = GEN::qk_idx();
+          const int32_t* rp = GEN::rj_ptr();
+          const int32_t* ri = GEN::rj_idx();
           for (int i = wave; i < n; i += NWAVE)
             for (int j = lane; j < n; j += 64) {  // wave per row i, lanes over j
             double acc = blk[GEN::OFF_P + j * n + i];
             if (i == j) acc += tol;
             for (int t = qp[i]; t < qp[i + 1]; ++t) {
               const int k = qi[t];
-              acc = fma(-blk[GEN::OFF_Q + k * n + i], RD[k * n + j], acc);
+              bool nz = false;
+              for (int u = rp[k]; u < rp[k + 1]; ++u) nz |= ri[u] == j;
+              if (nz) acc = fma(-blk[GEN::OFF_Q + k * n + i], RD[k * n + j], acc);
             }
             Am[(int64_t)i * ld + j] = acc;
           }

@@ -391,14 +391,20 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           w->sty[k] = ry * Di;
         }
         if (nl) {
-          /* nonlinear family: only Q's structural nonzeros K(i) enter S and rr
-             (structural zeros are exact zeros; a sparse elimination never touches them) */
+          /* nonlinear family: only the structural nonzeros enter S and rr — entry (i, j)
+             takes the terms k ∈ K(i) (Q's row pattern) with j ∈ J(k) (R's row pattern),
+             k ascending (structural zeros are exact zeros; a sparse elimination never
+             touches them) */
           for (int i = 0; i < n; ++i)
             for (int j = 0; j < n; ++j) {
               double acc = w->J[(size_t)i * N + j]; /* P_ij (+ tol) */
               for (int t = nl->qk_ptr[i]; t < nl->qk_ptr[i + 1]; ++t) {
                 const int k = nl->qk_idx[t];
-                acc = fma(-w->J[(size_t)i * N + n + k], w->J[(size_t)(n + k) * N + j] * w->sD[k], acc);
+                for (int u = nl->rj_ptr[k]; u < nl->rj_ptr[k + 1]; ++u)
+                  if (nl->rj_idx[u] == j) {
+                    acc = fma(-w->J[(size_t)i * N + n + k], w->J[(size_t)(n + k) * N + j] * w->sD[k], acc);
+                    break;
+                  }
               }
               w->Jr[(size_t)i * n + j] = acc;
             }

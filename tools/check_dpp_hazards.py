@@ -2,7 +2,8 @@
 
 1. Wait states.  A DPP instruction reading a VGPR that a VALU instruction wrote
    fewer than 2 wait states earlier reads a stale value (gfx9 hazard table);
-   v_readlane / v_readfirstlane need 1, v_permlane*_swap 2.  hipcc does not pad
+   v_readlane / v_readfirstlane need 1, v_permlane*_swap 2, and a v_writelane
+   whose lane-select SGPR a VALU wrote needs 4.  hipcc does not pad
    hazards whose consumer sits inside an asm statement.  For every such reader,
    walk back through the preceding instructions counting wait states (an
    instruction = 1, s_nop N = N+1) and flag a VALU write to its source.
@@ -31,6 +32,7 @@ import re
 import sys
 
 REG = re.compile(r"v\[(\d+):(\d+)\]|v(\d+)")
+SREG = re.compile(r"s\[(\d+):(\d+)\]|\bs(\d+)\b")
 NARROW = ("s_and_saveexec_b64", "s_andn2_saveexec_b64", "s_and_saveexec_b32")
 EXEC_WRITES = ("s_and_b64", "s_andn2_b64", "s_xor_b64", "s_or_b64", "s_mov_b64", "s_cselect_b64")
 
@@ -68,6 +70,24 @@ def parse(path: str):
     return out
 
 
+def sregs(tok: str) -> set:
+    out = set()
+    for m in SREG.finditer(tok):
+        if m.group(3) is not None:
+            out.add(int(m.group(3)))
+        else:
+            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
+    return out
+
+
+def valu_sdst(t: str) -> set:
+    """SGPRs a VALU instruction writes (v_readlane / v_readfirstlane / VOP3 compares)."""
+    o = t.split()[0]
+    if o.startswith("v_"):
+        return sregs(t[len(o):].split(",")[0])
+    return set()
+
+
 def valu_dst(t: str) -> set:
     o = t.split()[0]
     if o.startswith("v_") and not o.startswith(("v_readfirstlane", "v_readlane", "v_cmp")):
@@ -88,6 +108,25 @@ def wait_state_hazards(insts, want: str):
             src, need = regs(ops[1]), 1          # VALU write → v_readlane/readfirstlane: 1
         elif asm and op.startswith("v_permlane") and len(ops) >= 2:
             src, need = regs(ops[0]) | regs(ops[1]), 2
+        elif asm and op.startswith("v_writelane") and len(ops) >= 3:
+            # lane select written by a VALU: 4 wait states (VGPR sources: none)
+            checked += 1
+            sel, states, j = sregs(ops[2]), 0, i - 1
+            while j >= 0 and states < 4:
+                kk, tt, _, ll = insts[j]
+                if kk != k or ll:
+                    if ll:
+                        bad.append(f"WAIT-STATE HAZARD (join point {tt}) in {k}:\n   {t}")
+                    break
+                if tt.split()[0] == "s_nop":
+                    states += int(tt.split()[1], 0) + 1
+                elif valu_sdst(tt) & sel:
+                    bad.append(f"WAIT-STATE HAZARD in {k}:\n   {tt}\n   {t}  ({states} wait states between)")
+                    states += 1
+                else:
+                    states += 1
+                j -= 1
+            continue
         else:
             continue
         checked += 1
