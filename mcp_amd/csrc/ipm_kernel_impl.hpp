@@ -295,8 +295,10 @@ __device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, in
 // Dense LU with partial pivoting of the rows held in lanes [0, N) plus the
 // augmented right-hand side, then column-oriented back substitution.  On
 // success returns true and the solution entry of column `ln` in dz; returns
-// false if a pivot is exactly 0.  (A pivot-row broadcast through LDS instead of
-// SGPRs measured 24 % slower on the lone-wave lane-change LU, r02.)
+// false if a pivot is exactly 0.  Measured on the lone-wave lane-change LU (r02):
+// a pivot-row broadcast through LDS instead of SGPRs was 24 % slower, and a
+// look-ahead that starts step k+1's pivot search right after updating column k+1
+// (to overlap its DPP chain with the rest of the update) 4 % slower.
 template <int NMAX>
 __device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int N, int ln, double& dz) {
   uint64_t rem = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
