@@ -47,6 +47,11 @@
 #define MCPX_DPP_PAD_ON 0
 #endif
 
+// SCHUR kernels with compile-time (n, m) keep A, b, ϕ in LDS (A/B knob).
+#ifndef MCPX_LDS_A
+#define MCPX_LDS_A 1
+#endif
+
 // Waves per SIMD the register allocator targets in the SCHUR fast pass (A/B knob).
 #ifndef MCPX_FAST_WAVES
 #define MCPX_FAST_WAVES 5
@@ -374,22 +379,24 @@ __device__ __forceinline__ double dot_strided(const double* __restrict__ p, int 
 
 // SCHUR path (QP family), part 1: residuals.  x-lanes compute F_G, y-lanes
 // (which also own s_k) F_H and F_C; same fma order as family_row() of the
-// oracle.
+// oracle.  `ta` is the A block with leading dimension `lda` (A_ki = ta[i·lda + k]),
+// followed at ta[n·lda] by b and ϕ: θ itself (lda = m) or the wave's LDS copy.
 template <int BATCH>
-__device__ __forceinline__ void qp_residuals(const double* __restrict__ th, const double* zs, int ln, int n,
-                                             int m, double eps, double s_own, double& F, double& Fc) {
+__device__ __forceinline__ void qp_residuals(const double* __restrict__ th, const double* ta, int lda,
+                                             const double* zs, int ln, int n, int m, double eps, double s_own,
+                                             double& F, double& Fc) {
   const bool rg = ln < n, rh = ln >= n && ln < n + m;
-  const int kh = ln - n, nn = n * n, nm = n * m;
-  const double* px = rg ? th + ln : (rh ? th + nn + kh : th);
-  const int sx = rg ? n : (rh ? m : 0);
+  const int kh = ln - n, nl = n * lda;
+  const double* px = rg ? th + ln : (rh ? ta + kh : th);  // M column (θ) | A row
+  const int sx = rg ? n : (rh ? lda : 0);
   double acc = dot_strided<BATCH, false>(px, sx, zs, n, 0.0);  // M_ij x_j  |  A_kj x_j
-  const double acc_y = dot_strided<BATCH, true>(th + nn + (rg ? ln * m : 0), 1, zs + n, m, acc);  // − A_ki y_k
+  const double acc_y = dot_strided<BATCH, true>(ta + (rg ? ln * lda : 0), 1, zs + n, m, acc);  // − A_ki y_k
   if (rg) acc = acc_y;
   F = 0.0;
   Fc = 0.0;
-  if (rg) F = acc - th[nn + nm + m + ln];                       // G = Mx − Aᵀy − ϕ
+  if (rg) F = acc - ta[nl + m + ln];                            // G = Mx − Aᵀy − ϕ
   if (rh) {
-    F = (acc - th[nn + nm + kh]) - s_own;                       // H − s
+    F = (acc - ta[nl + kh]) - s_own;                            // H − s
     Fc = s_own * zs[n + kh] - eps;                              // s⊙y − ϵ
   }
 }
@@ -535,9 +542,11 @@ __device__ __forceinline__ void fmac_row_bcast_self(double& acc, double nl) {
 #undef MCPX_FMAC_NB_SELF
 
 // Transposed Schur complement in the 2-D layout (see above).  acc[I][J][r].
+// `ta` / `lda`: the A block as in qp_residuals.
 template <int NT>
-__device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, const double* sD, int ln, int n,
-                                                 int m, double tol, d4 (&acc)[NT][NT]) {
+__device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, const double* ta, int lda,
+                                                 const double* sD, int ln, int n, int m, double tol,
+                                                 d4 (&acc)[NT][NT]) {
   const int lr = ln >> 4, lc = ln & 15;
   {  // C = Mᵀ blocks: element (p = lr + 4r, q = lc) of tile (I, J) is M[16J+q][16I+p] = θ[(16I+p)·n + 16J+q]
     double mv[NT][NT][4];
@@ -562,11 +571,10 @@ __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, 
           acc[I][J][r] = in ? (row == col ? v + tol : v) : 0.0;  // M_ij (+ tol on the diagonal)
         }
   }
-  const int nn = n * n;
   const int kc = (m + 3) / 4;
   double nxt[NT];
 #pragma unroll
-  for (int X = 0; X < NT; ++X) nxt[X] = th[nn + min(16 * X + lc, n - 1) * m + min(lr, max(m - 1, 0))];
+  for (int X = 0; X < NT; ++X) nxt[X] = ta[min(16 * X + lc, n - 1) * lda + min(lr, max(m - 1, 0))];
   for (int c = 0; c < kc; ++c) {
     const int k = 4 * c + lr;
     const bool kin = k < m;
@@ -577,7 +585,7 @@ __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, 
     if (c + 1 < kc) {
       const int k1 = min(k + 4, m - 1);
 #pragma unroll
-      for (int X = 0; X < NT; ++X) nxt[X] = th[nn + min(16 * X + lc, n - 1) * m + k1];
+      for (int X = 0; X < NT; ++X) nxt[X] = ta[min(16 * X + lc, n - 1) * lda + k1];
     }
     double af[NT], bf[NT];
 #pragma unroll
@@ -751,6 +759,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   __shared__ double zs[64];
   __shared__ double sD[SCH ? 64 : 1], sT[SCH ? 64 : 1];  // SCHUR: D_k⁻¹, ty_k
   __shared__ double sB[SCH ? 64 : 1];  // rr, restored for the LU fallback
+  // SCHUR with compile-time (n, m): A (row i of Aᵀ at sA[i·LDA], odd stride: the
+  // lanes' row reads fall in different banks), b and ϕ copied into LDS once per
+  // instance; they are read five times per Newton step (residual rows of G and of H,
+  // rr, the Schur complement's MFMA fragments, δy), and from θ that traffic misses
+  // L2 (PMC).  M stays in θ: with it the copy would cap occupancy.
+  constexpr bool LDSA = SCH && NC > 0 && MC > 0 && MCPX_LDS_A;
+  constexpr int LDA = LDSA ? MC + 1 : 1;
+  __shared__ double sA[LDSA ? NC * LDA + MC + NC : 1];
   const int lane = threadIdx.x;
   const int64_t inst = blockIdx.x;
   const int n0 = NC ? NC : args.n, m0 = MC ? MC : args.m;
@@ -768,6 +784,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       if (RED) s = args.s0 ? args.s0[inst * m + (lane - n)] : 1.0;
     }
     if (!RED && lane >= n + m && lane < n + 2 * m) z = args.s0 ? args.s0[inst * m + (lane - n - m)] : 1.0;
+  }
+
+  if constexpr (LDSA) {  // read before the first step's barrier
+    const double* tg = th0 + NC * NC;
+#pragma unroll
+    for (int i = lane; i < NC * MC; i += 64) sA[(i / MC) * LDA + i % MC] = tg[i];
+    for (int i = lane; i < MC + NC; i += 64) sA[NC * LDA + i] = tg[NC * MC + i];
   }
 
   // SCHUR: M exactly symmetric ⇒ S symmetric ⇒ try the pivot-free SPD
@@ -815,6 +838,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       const int n = NC ? NC : opaque(n0), m = MC ? MC : opaque(m0);
       const int NS = SCH ? n : (RED ? n + m : n + 2 * m);  // rows of the linear system
       const double* __restrict__ th = th0 + opaque64(0);  // stays a global pointer
+      // SCHUR: the A block (then b, ϕ), from the wave's LDS copy when it has one
+      const double* const ta = LDSA ? (const double*)sA : th + n * n;
+      const int lda = LDSA ? LDA : m;
       const int ln = opaque_lane(lane);
       // ---- F!, ∇F_z! (:79-81) --------------------------------------------
       __syncthreads();
@@ -828,7 +854,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       // quotient-per-use form costs (8 of them in the Schur K-loop).
       double rw = 1.0, Di = 1.0, ryr = 0.0;
       if constexpr (SCH) {
-        qp_residuals<8>(th, zs, ln, n, m, eps, s, F, Fc);
+        qp_residuals<8>(th, ta, lda, zs, ln, n, m, eps, s, F, Fc);
         rhs = -F;
         if (rh) {  // eliminate δs_k (pivot w_k) and then δy_k (pivot D_k)
           w = zs[ln] + tol;
@@ -850,7 +876,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       if constexpr (SCH) {
         __syncthreads();
         // rr_i = −F_Gi + Σ_k A_ki ty_k  (x-lanes; other lanes' value unused)
-        rhs = dot_strided<8, false>(th + n * n + (ln < n ? ln : 0) * m, 1, sT, m, rhs);
+        rhs = dot_strided<8, false>(ta + (ln < n ? ln : 0) * lda, 1, sT, m, rhs);
         sB[ln] = rhs;
       }
       MCPX_STAMP(0);
@@ -864,7 +890,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         constexpr int NT = (NMAX + 15) / 16;
         if (spd_try) {  // S formed transposed on the matrix cores, Gauss-Jordan in that layout
           d4 acc4[NT][NT];
-          qp_schur_form_2d<NT>(th, sD, ln, n, m, tol, acc4);
+          qp_schur_form_2d<NT>(th, ta, lda, sD, ln, n, m, tol, acc4);
           double acc[NT][NT][4];
 #pragma unroll
           for (int I = 0; I < NT; ++I)
@@ -892,7 +918,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
           // ds_bpermute: no n×n LDS tile, so LDS (2 KB per wave) does not cap occupancy
           constexpr int NT = (NMAX + 15) / 16;
           d4 acc4[NT][NT];
-          qp_schur_form_2d<NT>(th, sD, ln, n, m, tol, acc4);
+          qp_schur_form_2d<NT>(th, ta, lda, sD, ln, n, m, tol, acc4);
           schur_rows_from_2d<NT, NMAX>(acc4, ln, n, a);
           rhs = sB[ln];
           ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
@@ -909,7 +935,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         __syncthreads();
         zs[ln] = dz;
         __syncthreads();
-        const double acc = dot_strided<8, true>(th + n * n + (rh ? ln - n : 0), m, zs, n, ryr);
+        const double acc = dot_strided<8, true>(ta + (rh ? ln - n : 0), lda, zs, n, ryr);
         // branch-free consumer: under `if (rh)` the compiler sinks all n loads of
         // the dot into that block at once (n more live registers)
         const double dzy = acc * Di;
