@@ -132,6 +132,28 @@ __device__ __forceinline__ double wave_max_nonneg(double v) {
   return __hiloint2double((int)mhi, (int)mlo);
 }
 
+// 1 / b, correctly rounded (== the IEEE quotient the oracle's C division takes),
+// for a wave-uniform b.  The compiler's f64 division is v_div_scale ×2, v_rcp,
+// two Newton steps, a product, the remainder, v_div_fmas and v_div_fixup: 11
+// VALU instructions.  For 2⁻⁵⁰⁰ ≤ |b| ≤ 2⁵⁰⁰ (numerator 1) the scales are the
+// identity, v_div_fmas is a plain fma and v_div_fixup returns its input, so the
+// same chain without them (7 instructions) gives the same bits; other b (0,
+// subnormal, huge, Inf, NaN) take the full division.  The test is on the SGPR
+// copy of b, so the branch is scalar.
+__device__ __forceinline__ double rcp_uniform(double b) {
+  const uint32_t e = ((uint32_t)__double2hiint(b) >> 20) & 0x7ffu;  // biased exponent
+  if (__builtin_expect(e - 523u <= 1000u, 1)) {
+    double y = __builtin_amdgcn_rcp(b);
+    double t = fma(-b, y, 1.0);
+    y = fma(y, t, y);
+    t = fma(-b, y, 1.0);
+    y = fma(y, t, y);
+    t = fma(-b, y, 1.0);  // remainder of the quotient 1·y
+    return fma(t, y, y);
+  }
+  return 1.0 / b;
+}
+
 // NaN-propagating max (Julia `max`, as in norm(F, Inf), src/solver.jl:107)
 __device__ __forceinline__ double max_nan(double a, double b) { return (a != a || b != b) ? a + b : fmax(a, b); }
 
@@ -625,7 +647,7 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
     const int Ik = Ck >> 2, rk = Ck & 3;       // local column Ck = accumulator tile Ik, element rk
     const double piv = bcast(acc[Ik][Jk][rk], 16 * Qk + Rk);
     bad |= !(piv > 0.0);
-    const double rp = 1.0 / piv;  // oracle gj_spd_solve: l_i = a_ik · (1 / a_kk)
+    const double rp = rcp_uniform(piv);  // oracle gj_spd_solve: l_i = a_ik · (1 / a_kk)
     const bool prow = lc == Rk;  // this lane holds the pivot row in half Jk
     if (prow) dg[Jk] = piv;
     double nl[NT];
