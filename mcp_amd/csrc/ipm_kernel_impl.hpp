@@ -293,7 +293,7 @@ __device__ __forceinline__ void assemble_row(const double* __restrict__ th, cons
 template <int NMAX>
 __device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, int k, double l, uint64_t pm,
                                               bool upd) {
-  constexpr int G = 16;  // columns per EXEC-masked broadcast
+  constexpr int G = 16;  // columns per EXEC-masked broadcast (8: 2-4 % slower on C4, r02 A/B)
   // columns k+1 .. NMAX-1 and the right-hand side (index NMAX)
 #pragma clang loop unroll(full)
   for (int g = 0; g <= NMAX / G; ++g) {
@@ -323,47 +323,77 @@ __device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, in
 // augmented right-hand side, then column-oriented back substitution.  On
 // success returns true and the solution entry of column `ln` in dz; returns
 // false if a pivot is exactly 0.  Measured on the lone-wave lane-change LU (r02):
-// a pivot-row broadcast through LDS instead of SGPRs was 24 % slower, and a
+// a pivot-row broadcast through LDS instead of SGPRs was 24 % slower (30-45 % in a
+// second A/B, profiles/r02/ab_c4_lu_variants.txt), and a
 // look-ahead that starts step k+1's pivot search right after updating column k+1
 // (to overlap its DPP chain with the rest of the update) 4 % slower.
+//
+// Guessed pivots (`spec`, the nonlinear SCHUR kernel): lane k of `pk` holds on entry
+// the pivot row of step k of an earlier factorisation (the previous Newton step's).
+// Step k then skips the pivot search and only checks, lane by lane, that the
+// first-max rule above would have picked the guessed row; the arithmetic is the
+// searched LU's, so when every check holds the bits are the same.  A failed check,
+// or a guessed pivot that is 0 or NaN (singular / all-NaN cases the search decides),
+// sets `miss`: the caller restores the rows and runs the search.
+#ifndef MCPX_LU_NO_SPEC
+#define MCPX_LU_NO_SPEC 0
+#endif
 template <int NMAX>
-__device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int N, int ln, double& dz) {
+__device__ __forceinline__ bool lu_solve_rows_core(double (&a)[NMAX], double rhs, int N, int ln, double& dz,
+                                                   int& pk, bool spec, bool& miss) {
   uint64_t rem = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
   int my_step = 1 << 30;  // LU step at which this row became a pivot row
-  int pk = 0;             // lane k: pivot row of step k
   bool singular = false;
+  bool viol = false;  // spec: a remaining row beats the guessed pivot under the first-max rule
+  miss = false;
 #pragma clang loop unroll(full)
   for (int k = 0; k < NMAX; ++k) {
     if (k >= N || singular) continue;  // uniform; no `break` so the loop fully unrolls
     const double ak = a[k];
     const double av = fabs(ak);
-    const bool valid = ((rem >> ln) & 1ull) && !(av != av);
-    const uint32_t khi = valid ? (uint32_t)__double2hiint(av) + 1u : 0u;
-    const uint32_t mhi = wave_max_u32(khi);
     int p;
-    if (mhi == 0u) {
-      p = lowest_lane(rem);  // every remaining entry is NaN
-    } else {
-      const uint64_t cand = ballot(khi == mhi);
-      if (__popcll(cand) == 1) {
-        p = lowest_lane(cand);
-      } else {  // exact tie-break on the low word, lowest lane wins
-        const uint32_t klo = (khi == mhi) ? (uint32_t)__double2loint(av) : 0u;
-        const uint32_t mlo = wave_max_u32(klo);
-        p = lowest_lane(ballot(khi == mhi && klo == mlo));
+    double piv;
+    if (spec && !MCPX_LU_NO_SPEC) {
+      p = __builtin_amdgcn_readlane(pk, k);
+      piv = bcast(ak, p);
+      const double ap = fabs(piv);
+      if (!(ap > 0.0)) {  // 0 or NaN: let the search decide
+        miss = true;
+        singular = true;
+        continue;
       }
-    }
-    const double piv = bcast(ak, p);
-    if (piv == 0.0) {  // singular: the failed linear solve of src/solver.jl:84-88
-      singular = true;
-      continue;
+      // NaN entries never win the search (av > ap is false for them); bitwise, no branches
+      const bool beats = (av > ap) | ((av == ap) & (ln < p));
+      viol = viol | ((((rem >> ln) & 1ull) != 0) & (ln != p) & beats);
+    } else {
+      const bool valid = ((rem >> ln) & 1ull) && !(av != av);
+      const uint32_t khi = valid ? (uint32_t)__double2hiint(av) + 1u : 0u;
+      const uint32_t mhi = wave_max_u32(khi);
+      if (mhi == 0u) {
+        p = lowest_lane(rem);  // every remaining entry is NaN
+      } else {
+        const uint64_t cand = ballot(khi == mhi);
+        if (__popcll(cand) == 1) {
+          p = lowest_lane(cand);
+        } else {  // exact tie-break on the low word, lowest lane wins
+          const uint32_t klo = (khi == mhi) ? (uint32_t)__double2loint(av) : 0u;
+          const uint32_t mlo = wave_max_u32(klo);
+          p = lowest_lane(ballot(khi == mhi && klo == mlo));
+        }
+      }
+      piv = bcast(ak, p);
+      if (piv == 0.0) {  // singular: the failed linear solve of src/solver.jl:84-88
+        singular = true;
+        continue;
+      }
     }
     rem &= ~(1ull << p);
     if (ln == p) my_step = k;
     if (ln == k) pk = p;
     eliminate_row<NMAX>(a, rhs, k, ak / piv, 1ull << p, (rem >> ln) & 1ull);
   }
-  if (singular) return false;
+  if (spec && ballot(viol)) miss = true;
+  if (singular || miss) return false;
   dz = 0.0;
 #pragma clang loop unroll(full)
   for (int k = NMAX - 1; k >= 0; --k) {
@@ -376,6 +406,13 @@ __device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int
     }
   }
   return true;
+}
+
+template <int NMAX>
+__device__ __forceinline__ bool lu_solve_rows(double (&a)[NMAX], double rhs, int N, int ln, double& dz) {
+  int pk = 0;
+  bool miss;
+  return lu_solve_rows_core<NMAX>(a, rhs, N, ln, dz, pk, false, miss);
 }
 
 typedef double d4 __attribute__((ext_vector_type(4)));

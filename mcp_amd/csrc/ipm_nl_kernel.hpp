@@ -94,6 +94,8 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   int status = 0;                     // :69
   int outer = 1;                      // :70
   int newton = 0;
+  int piv_guess = 0;        // SCHUR: lane k = pivot row of LU step k at the last Newton step
+  bool have_guess = false;  // (lu_solve_rows_core)
 #if MCPX_STAMPS
   uint64_t st_acc[4] = {0, 0, 0, 0};
   uint64_t st_last = __builtin_amdgcn_s_memtime();
@@ -176,7 +178,26 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
           for (int j = 0; j < n; ++j) a[j] = row[j];
         }
         MCPX_STAMP(1);
-        ok = lu_solve_rows<NMAX>(a, rhs, opaque(n), lane, dz);
+        // LU of S with the previous Newton step's pivot sequence as the guess (the
+        // lane-change game keeps it on 86 % of steps); a missed guess restores the rows
+        // from Srow and factors again with the pivot search.  Bits equal the searched LU.
+        bool spec = have_guess, miss;
+        for (;;) {
+          if (spec && lx) {
+            double* row = Srow + i * LDR;
+#pragma unroll
+            for (int j = 0; j < n; ++j) row[j] = a[j];
+            row[n] = rhs;
+          }
+          ok = lu_solve_rows_core<NMAX>(a, rhs, opaque(n), lane, dz, piv_guess, spec, miss);
+          if (!miss) break;
+          const double* row = Srow + i * LDR;
+#pragma unroll
+          for (int j = 0; j < NMAX; ++j) a[j] = (j < n) ? row[j] : 0.0;
+          rhs = lx ? row[n] : 0.0;
+          spec = false;
+        }
+        have_guess = ok;
         MCPX_STAMP(2);
         if (ok) {
           if (lx) dzs[lane] = dz;
