@@ -196,3 +196,32 @@ def test_gpu_lane_change_api_device_path(gpu, lane, oracle_lib):
     ref = oracle_lib.solve_batch_nl(mcp.nl, mcp.theta_map(th), x0=x0, linear_solver="schur", nthreads=8)
     np.testing.assert_array_equal(sol.x.cpu().numpy(), ref["x"])
     np.testing.assert_array_equal(sol.status.cpu().numpy(), ref["status"])
+
+
+@pytest.mark.gpu
+def test_gpu_lane_change_c4_batch_and_edge_inputs(gpu, lane, oracle_lib):
+    """The BASELINE C4 batch itself (1,024 games of the bench's θ stream, 45-50 of which run
+    all 931 Newton steps) plus games with NaN / Inf / huge / zeroed parameters, bit-exact vs
+    the oracle.  Exercises the guessed-pivot LU of mcpx_nl_solve_schur on every path: guesses
+    that hold, guesses that miss (re-factored with the search), and NaN or zero guessed
+    pivots (csrc/ipm_kernel_impl.hpp, lu_solve_rows_core)."""
+    from mcp_amd.batch import solve_batch
+    from mcp_amd.qp_benchmark import chunked_slice
+
+    mcp = lane.mcp
+    th = chunked_slice(lambda rng, k: lane.generate_random_parameter(rng, k), 1, 0, 1024)
+    edge = np.repeat(th[:1], 8, 0)
+    edge[0, 0] = np.nan
+    edge[1, 3] = np.inf
+    edge[2, :] = 0.0
+    edge[3, 1] = 1e200
+    edge[4, 5] = -1e-300
+    edge[5, :4] = edge[5, 5:9]  # both players start in the same state
+    edge[6, 2] = -np.inf
+    edge[7, 9] = 1e6
+    th = np.concatenate([th, edge])
+    tp = np.ascontiguousarray(mcp.theta_map(th))
+    got = solve_batch(_abi.FAMILY_NONLINEAR, 40, 50, tp, linear_solver="schur", trace_len=TRACE, module=mcp.module())
+    ref = oracle_lib.solve_batch_nl(mcp.nl, tp, linear_solver="schur", trace_len=TRACE, nthreads=8)
+    assert_parity(got, ref)
+    assert (ref["newton_iters"][:1024] == 931).sum() >= 30  # the tail really ran
