@@ -129,8 +129,8 @@ def host_cpus() -> dict:
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--global-batch", type=int, default=0,
                     help="instances over all GPUs, sharded (strong scaling); 0 = the BASELINE config's")
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU (weak scaling) instead")
