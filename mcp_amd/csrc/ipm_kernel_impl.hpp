@@ -1011,11 +1011,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       const double cvy = args.c_tau * z, cvs = args.c_tau * sv;
       uint64_t vs = 0ull, vy = 0ull;
       double alpha = 1.0;
+      bool clean_s = false, clean_y = false;  // a trial without violation seen (uniform)
       for (int e = 0; e < args.n_trials; ++e) {
         const double ty = alpha * dz, ts = alpha * sd;
         const double ly = z + ty, ls = sv + ts;
-        if (ballot(rs && ls < cvs)) vs |= 1ull << e;
-        if (ballot(ry && ly < cvy)) vy |= 1ull << e;
+        const bool bs = ballot(rs && ls < cvs) != 0ull, by = ballot(ry && ly < cvy) != 0ull;
+        if (bs) vs |= 1ull << e;
+        if (by) vy |= 1ull << e;
+        clean_s = clean_s || !bs;
+        clean_y = clean_y || !by;
+        // e_s / e_y are the lowest clear bits: once both exist, later trials cannot move them
+        if (clean_s && clean_y) break;
         alpha *= args.decay;
       }
       const int es = (~vs) ? lowest_lane(~vs) : 64;

@@ -307,6 +307,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
       }
       uint64_t vs = 0ull, vy = 0ull;
       double alpha = 1.0;
+      bool clean_s = false, clean_y = false;  // a trial without violation seen (uniform)
       for (int e = 0; e < args.n_trials; ++e) {
         bool bs = false, by = false;
 #pragma unroll
@@ -316,8 +317,13 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
             by = by || (yv[r] + alpha * dyv[r] < args.c_tau * yv[r]);
           }
         }
-        if (ballot(bs)) vs |= 1ull << e;
-        if (ballot(by)) vy |= 1ull << e;
+        const bool ws = ballot(bs) != 0ull, wy = ballot(by) != 0ull;
+        if (ws) vs |= 1ull << e;
+        if (wy) vy |= 1ull << e;
+        clean_s = clean_s || !ws;
+        clean_y = clean_y || !wy;
+        // e_s / e_y are the lowest clear bits: once both exist, later trials cannot move them
+        if (clean_s && clean_y) break;
         alpha *= args.decay;
       }
       const int es = (~vs) ? lowest_lane(~vs) : 64;
