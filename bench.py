@@ -45,8 +45,10 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (MI355X_MICROAR
 HBM_PEAK_GBS = 8000.0
 XCDS, SIMDS = 8, 256 * 4  # MI355X: 8 XCDs, 256 CUs × 4 SIMDs
 # rocprofv3 evidence of this round's kernels (tools/gpu_profile.sh + tools/prof_summary.py)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
 DEFAULT_GLOBAL = {"c3": 65536, "c5": 4096, "c4": 1024}
+QP_FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters")
+C4_FIELDS = QP_FIELDS
 
 
 def lu_flops(N: int) -> float:
@@ -95,10 +97,67 @@ def one_wave(n: int, m: int, linear_solver: str) -> bool:
     return solve_dim(n, m, linear_solver) <= 64 and lanes <= 64
 
 
-def roofline_bound(linear_solver: str) -> str:
-    """What limits the solve kernels (PMC evidence): the register LU /
-    Gauss-Jordan is FP64-VALU-issue-bound; θ traffic is ≤ 1/5 of HBM peak."""
-    return "valu"
+def roofline_bound(ev: dict, kern_ms: float, fallback: str) -> tuple:
+    """What limits the kernel, from the committed PMC counters of this configuration and
+    build (tools/gpu_profile.sh): the largest of
+      hbm  = (FETCH_SIZE + WRITE_SIZE) / kernel time / 8 TB/s,
+      mfma = MFMA-busy SIMD-cycles / (active cycles × SIMDs),
+      valu = SQ_INSTS_VALU × 4 cycles (a wave64 VALU op, FP64 at full rate) / (active cycles × SIMDs);
+    "latency" when none reaches 0.3 (waves stall on dependencies, not on a unit).  Without
+    PMC evidence for this build: `fallback`, marked as such."""
+    p = ev.get("pmc") or {}
+    if not p.get("GRBM_GUI_ACTIVE"):
+        return fallback, {"source": "assumed: no PMC summary of this configuration and build"}
+    sim_cycles = p["GRBM_GUI_ACTIVE"] / XCDS * SIMDS
+    fr = {}
+    if "FETCH_SIZE" in p and "WRITE_SIZE" in p:
+        fr["hbm"] = (p["FETCH_SIZE"] + p["WRITE_SIZE"]) * 1024.0 / (kern_ms * 1e-3) / (HBM_PEAK_GBS * 1e9)
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in p:
+        fr["mfma"] = p["SQ_VALU_MFMA_BUSY_CYCLES"] / sim_cycles
+    if "SQ_INSTS_VALU" in p:
+        fr["valu"] = p["SQ_INSTS_VALU"] * 4.0 / sim_cycles
+    best = max(fr, key=fr.get) if fr else fallback
+    bound = best if fr and fr[best] >= 0.3 else "latency"
+    return bound, {"source": p.get("_source"), "utilisation": fr}
+
+
+def parity_report(got: dict, ref: dict, fields, count: int, what: str) -> dict:
+    """Bit-exact comparison of the GPU outputs of the first `count` instances with the
+    oracle's (parity pass/fail in every bench line): per field the
+    number of instances with any differing entry (NaN = NaN)."""
+    mism = {}
+    for f in fields:
+        g = np.asarray(got[f])[:count]
+        r = np.asarray(ref[f])[:count]
+        same = (g == r)
+        if np.issubdtype(g.dtype, np.floating):
+            same |= np.isnan(g) & np.isnan(r)
+        mism[f] = int((~same.reshape(count, -1).all(1)).sum())
+    return {"instances": int(count), "bit_exact_fields": [f for f in fields if mism[f] == 0],
+            "mismatches": mism, "pass": all(v == 0 for v in mism.values()), "reference": what}
+
+
+def fixture_parity() -> dict:
+    """The committed golden vectors of the QP family (tests/golden/qp_*.npz, readme_qp*.npz:
+    inputs and the oracle's outputs, tests/golden/make_golden.py) through the GPU host API,
+    bit-exact on every output field."""
+    import glob
+
+    from mcp_amd.batch import solve_batch
+
+    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "qp_*.npz"))
+                   + glob.glob(os.path.join(ROOT, "tests", "golden", "readme_qp*.npz")))
+    bad, inst = [], 0
+    fields = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters")
+    for f in files:
+        d = np.load(f, allow_pickle=False)
+        kw = {k[len("param_"):]: d[k].item() for k in d.files if k.startswith("param_")}
+        got = solve_batch(int(d["family"]), int(d["n"]), int(d["m"]), d["theta"], num_devices=1, **kw)
+        rep = parity_report(got, {k: d["out_" + k] for k in fields}, fields, d["theta"].shape[0], "")
+        inst += rep["instances"]
+        if not rep["pass"]:
+            bad.append(os.path.basename(f))
+    return {"files": len(files), "instances": inst, "failed_files": bad, "pass": not bad and bool(files)}
 
 
 def host_cpus() -> dict:
@@ -306,12 +365,16 @@ def reduce_max_sum(dist, dev, world, maxes, sums):
 
 
 def roofline(kern_ms: float, flops_launch: float, exec_flops_launch: float, alg_bytes: float, ev: dict,
-             kernel: str, bound: str, note: str) -> dict:
+             kernel: str, bound, note: str) -> dict:
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
     executed = exec_flops_launch / (kern_ms * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(ev)
-    r = {"bound": bound, "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+    bound, bound_ev = bound
+    r = {"bound": bound, "bound_evidence": bound_ev, "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
+         "frac_basis": "algorithmic: SURVEY.md §8(d) dense-LU FLOPs of the full KKT system (not the FLOPs the "
+                       "kernel executes: executed_frac)",
+         "traffic": traffic, "traffic_source": traffic_src,
          "executed_tflops": executed, "executed_frac": executed / FP64_PEAK_TFLOPS,
          "algorithmic_bytes": alg_bytes, "hbm_gbs_algorithmic": alg_bytes / (kern_ms * 1e-3) / 1e9,
          "kernel": kernel, "kernel_ms": kern_ms, "flops_per_launch": flops_launch,
@@ -383,7 +446,7 @@ def main_lane_change(a, world, rank, local, dist, pl):
     ev = evidence(key, cfg)
     kernel = "mcpx_nl_solve_" + ls + ("" if mcp.nl.solvers()[ls] else "_wg")
     rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops_nl(mcp.nl, ls),
-                  B * 8.0 * (mcp.nl.p + n + 2 * m + 2) + 12.0 * B, ev, kernel, "latency",
+                  B * 8.0 * (mcp.nl.p + n + 2 * m + 2) + 12.0 * B, ev, kernel, roofline_bound(ev, kern_ms, "latency"),
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system per Newton step) "
                   f"x rank 0's own Newton counts / HIP-event kernel time; executed = the linear solve the kernel "
                   f"performs ({ls}: LU of dim {solve_dim(n, m, ls)}" + (" + the Schur complement from Q's structural "
@@ -415,7 +478,10 @@ def main_lane_change(a, world, rank, local, dist, pl):
                           B, a, th, "C oracle with the generated host G/H code (same algorithm and linear solver)",
                           per_thread=256 if a.lane_change <= 2 else 4)
         r = cb.pop("_result")
-        cb["status_match"] = bool(np.array_equal(r["status"], out["status"][:len(r["status"])].cpu().numpy()))
+        k = len(r["status"])
+        got = {f: out[f][:k].cpu().numpy() for f in C4_FIELDS}
+        res["parity"] = parity_report(got, r, C4_FIELDS, k, "oracle/ipm_oracle.c with the same generated G/H "
+                                      "code (cpu_baseline sample)")
         res["cpu_baseline"] = cb
     print(json.dumps(res), flush=True)
 
@@ -529,7 +595,8 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     p = n * n + m * n + m + n
     rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
                   B * (8.0 * (p + n + 2 * m + 2) + 12.0), ev,
-                  "ipm_solve_kernel" if one_wave(n, m, ls) else "ipm_wg_kernel_t", roofline_bound(ls),
+                  "ipm_solve_kernel" if one_wave(n, m, ls) else "ipm_wg_kernel_t",
+                  roofline_bound(ev, kern_ms, "valu" if one_wave(n, m, ls) else "hbm"),
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system, 2N^3/3+2N^2 per "
                   f"Newton step) x rank 0's own Newton counts / HIP-event time of the solve launch; executed = the FP64 "
                   f"work the kernel performs per step (residual + " + ("MFMA Schur complement + Gauss-Jordan of the "
@@ -550,7 +617,8 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         "dtype": "f64",
         "data": "synthetic (random dense QPs of benchmark/quadratic_program_benchmark.jl, host numpy PCG64 in chunks "
                 f"of 4096 seeded SeedSequence({a.seed}, spawn_key=(chunk,)), uploaded to HBM before timing)",
-        "config": {"workload": (f"BASELINE {'C5' if a.sens else 'C3'}: random dense QP-KKT n={n} m={m} (KKT dim {N}), "
+        "config": {"workload": (f"BASELINE {'C5' if a.sens else ('C2' if (n, m) == (16, 8) else 'C3')}: random dense "
+                                f"QP-KKT n={n} m={m} (KKT dim {N}), "
                                 f"fp64, global batch {G} ({B} on rank 0), tol={a.tol:g}"
                                 + (", solve + rrule pullback (VJP kernel) of f = Σx²+Σy²" if a.sens else "")),
                    "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "solve_dim": NS,
@@ -590,7 +658,21 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
                           B, a, th, "C oracle (oracle/ipm_oracle.c, same algorithm and linear solver)")
         r = cb.pop("_result")
         cb["newton_mean"] = float(r["newton_iters"].mean())
+        k = len(r["status"])
+        got = {f: out[f][:k].cpu().numpy() for f in QP_FIELDS}
+        res["parity"] = parity_report(got, r, QP_FIELDS, k, "oracle/ipm_oracle.c, same linear solver "
+                                      "(cpu_baseline sample)")
+        if a.sens:  # the pullback of the same instances against oracle_vjp_batch
+            kv = min(k, 1024)
+            x, y, s_ = (out[f][:kv].cpu().numpy() for f in ("x", "y", "s"))
+            rd, rs = coracle.vjp_batch(0, n, m, theta_host[:kv], x, y, s_, 2.0 * x, 2.0 * y, np.zeros_like(y),
+                                       nthreads=th)
+            res["parity"]["vjp"] = parity_report({"dtheta": dtheta[:kv].cpu().numpy(), "status": vstat[:kv].cpu().numpy()},
+                                                 {"dtheta": rd, "status": rs}, ("dtheta", "status"), kv,
+                                                 "oracle_vjp_batch on the GPU's solutions")
         res["cpu_baseline"] = cb
+    if world == 1 and not a.sens:
+        res["parity_fixtures"] = fixture_parity()
     print(json.dumps(res), flush=True)
 
 

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MCPX_VERSION 10300 /* 1.3.0 */
+#define MCPX_VERSION 10400 /* 1.4.0 */
 
 /* error codes */
 #define MCPX_OK 0
@@ -101,11 +101,16 @@ extern "C" {
  *                         Schur complement (default; N ≤ 64 means n + m ≤ 64);
  *  MCPX_LINSOLVE_DENSE    dense LU with partial pivoting of the full
  *                         (n+2m)-dim system (n + 2m ≤ 64);
- *  MCPX_LINSOLVE_SCHUR    QP family only (∂H/∂y = 0): after the slack block,
- *                         the now-diagonal y block is eliminated as well and
- *                         the n×n Schur complement (M + tol·I) + Aᵀ D⁻¹ A is
- *                         formed on the matrix cores (fp64 MFMA) and solved by
- *                         dense LU with partial pivoting (n + m ≤ 64). */
+ *  MCPX_LINSOLVE_SCHUR    ∂H/∂y = 0 (QP family; generated modules without an
+ *                         ∂H/∂y block): after the slack block, the now-diagonal
+ *                         y block is eliminated as well, leaving the n×n Schur
+ *                         complement S = (M + tol·I) + Aᵀ D⁻¹ A (QP: formed on
+ *                         the matrix cores, fp64 MFMA).  QP with M exactly
+ *                         symmetric: S is solved by pivot-free Gauss-Jordan
+ *                         while every pivot is > 0 (S SPD), and by dense LU with
+ *                         partial pivoting otherwise — the oracle takes the same
+ *                         branch (gj_spd_solve / lu_solve); modules: dense LU with
+ *                         partial pivoting.  One wave: n + m ≤ 64. */
 #define MCPX_LINSOLVE_REDUCED 0
 #define MCPX_LINSOLVE_DENSE 1
 #define MCPX_LINSOLVE_SCHUR 2
@@ -201,9 +206,11 @@ int mcpx_solve_batch_device(const mcpx_desc* desc, const double* theta,
  *     ∂z/∂θ = −(∇F_z)⁻¹ ∇F_θ      (src/AutoDiff.jl:18-40; `qr(−∇F_z, ColumnNorm()) \ ∇F_θ`)
  * with ∇F_z WITHOUT the tol·I regularisation, at the final (x, y, s)
  * (SURVEY.md Appendix A.10).  For both families ∇F_z and ∇F_θ do not depend on ϵ.
- * The kernels solve the same square system by dense LU with partial pivoting
- * of the full (n+2m)-dim ∇F_z (or its transpose); for a nonsingular ∇F_z that
- * equals the reference's pivoted-QR solve up to rounding.  An exactly zero
+ * The kernels solve the same square system by dense LU with partial pivoting:
+ * the JVP factors the full (n+2m)-dim ∇F_z, the VJP the (n+m)-dim system left
+ * after eliminating λ_s of ∇F_zᵀ exactly through its −1 entries (no division);
+ * for a nonsingular ∇F_z that equals the reference's pivoted-QR solve up to
+ * rounding (amplified by cond(∇F_z), which is large at degenerate solutions).  An exactly zero
  * pivot (∇F_z singular, where the reference's QR would return a basic
  * least-squares solution) is reported per instance: status[b] = 1 and the
  * instance's outputs are NaN.
@@ -214,7 +221,10 @@ int mcpx_solve_batch_device(const mcpx_desc* desc, const double* theta,
  * gx [B*n], gy [B*m], gs [B*m] (any of gx/gy/gs may be NULL = zero cotangent,
  * ChainRulesCore's ZeroTangent).  Output: dtheta [B*p] (p = mcpx_theta_dim,
  * dense stride p, the family's θ layout), status [B] or NULL.
- * Needs n + 2m <= MCPX_MAX_KKT_DIM. */
+ * n + 2m <= MCPX_MAX_KKT_DIM runs one wave per instance (the system in registers),
+ * larger systems up to MCPX_MAX_WG_KKT_DIM one workgroup per instance (the
+ * system in an HBM workspace, blocked LU with MFMA trailing updates); both give
+ * the same bits. */
 int mcpx_vjp_batch(const mcpx_desc* desc, const double* theta, const double* x, const double* y,
                    const double* s, const double* gx, const double* gy, const double* gs,
                    int num_devices, double* dtheta, int32_t* status);
@@ -253,12 +263,16 @@ int mcpx_jvp_batch_device(const mcpx_desc* desc, const double* theta, const doub
  * another linear_solver is MCPX_EUNSUPPORTED.
  */
 typedef struct mcpx_module mcpx_module;
+/* Sensitivity kernels of a module (bits of the mcpx_module_dims kernel mask) */
+#define MCPX_MODULE_VJP 6
+#define MCPX_MODULE_JVP 7
 /* Loads the code object at `path` on the current device (other devices load
  * it on first use).  No usable GPU: MCPX_ENODEV. */
 int mcpx_module_load(const char* path, mcpx_module** mod);
 /* The module's n, m, θ dimension p and kernel mask: bit MCPX_LINSOLVE_* for the
- * one-wave kernels, bit 3 + MCPX_LINSOLVE_* for the workgroup kernels; NULL
- * pointers are skipped. */
+ * one-wave kernels, bit 3 + MCPX_LINSOLVE_* for the workgroup kernels, bits
+ * MCPX_MODULE_VJP / MCPX_MODULE_JVP for the sensitivity kernels; NULL pointers
+ * are skipped. */
 int mcpx_module_dims(const mcpx_module* mod, int32_t* n, int32_t* m, int32_t* p, int32_t* solvers);
 void mcpx_module_unload(mcpx_module* mod);
 /* mcpx_solve_batch / mcpx_solve_batch_device for the module's problem:
@@ -269,6 +283,28 @@ int mcpx_solve_batch_module(mcpx_module* mod, const mcpx_desc* desc, const doubl
 int mcpx_solve_batch_module_device(mcpx_module* mod, const mcpx_desc* desc, const double* theta,
                                    const double* x0, const double* y0, const double* s0,
                                    const mcpx_params* prm, const mcpx_out* out, void* stream);
+
+/* Sensitivities of the module's problem — the rrule pullback and the Dual method of
+ * src/AutoDiff.jl for any PrimalDualMCP built with compute_sensitivities = true
+ * (src/mcp.jl:122-147: ∇F_θ from the generated mcpx_nl_eval_theta), e.g. the
+ * trajectory games of src/game.jl.  Same argument meaning as mcpx_vjp_batch /
+ * mcpx_jvp_batch with p = the module's θ dimension; one workgroup per instance
+ * (VJP: the (n+m)-dim reduced ∇F_zᵀ system, JVP: the (n+2m)-dim ∇F_z, blocked LU
+ * with partial pivoting).  MCPX_EUNSUPPORTED when the module has no such kernel
+ * (mask bits MCPX_MODULE_VJP / MCPX_MODULE_JVP). */
+int mcpx_vjp_batch_module(mcpx_module* mod, const mcpx_desc* desc, const double* theta, const double* x,
+                          const double* y, const double* s, const double* gx, const double* gy,
+                          const double* gs, int num_devices, double* dtheta, int32_t* status);
+int mcpx_vjp_batch_module_device(mcpx_module* mod, const mcpx_desc* desc, const double* theta,
+                                 const double* x, const double* y, const double* s, const double* gx,
+                                 const double* gy, const double* gs, double* dtheta, int32_t* status,
+                                 void* stream);
+int mcpx_jvp_batch_module(mcpx_module* mod, const mcpx_desc* desc, const double* theta, const double* x,
+                          const double* y, const double* s, int32_t n_partials, const double* theta_dot,
+                          int num_devices, double* zdot, int32_t* status);
+int mcpx_jvp_batch_module_device(mcpx_module* mod, const mcpx_desc* desc, const double* theta,
+                                 const double* x, const double* y, const double* s, int32_t n_partials,
+                                 const double* theta_dot, double* zdot, int32_t* status, void* stream);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,7 @@ MAX_WG_KKT_DIM = 768  # MCPX_MAX_WG_KKT_DIM: workgroup-per-instance kernels (QP 
 KERNEL_AUTO, KERNEL_WAVE, KERNEL_WORKGROUP = 0, 1, 2
 KERNELS = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "workgroup": KERNEL_WORKGROUP}
 JVP_RHS = 8  # MCPX_JVP_RHS: partials per factorisation of the JVP kernel
+MODULE_VJP, MODULE_JVP = 6, 7  # MCPX_MODULE_VJP / _JVP: sensitivity-kernel bits of a module's kernel mask
 
 LINSOLVE_REDUCED = 0
 LINSOLVE_DENSE = 1

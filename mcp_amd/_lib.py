@@ -29,7 +29,8 @@ EXPORTS = ("mcpx_version", "mcpx_last_error", "mcpx_default_params", "mcpx_theta
            "mcpx_device_count", "mcpx_solve_batch", "mcpx_solve_batch_device", "mcpx_vjp_batch",
            "mcpx_vjp_batch_device", "mcpx_jvp_batch", "mcpx_jvp_batch_device", "mcpx_module_load",
            "mcpx_module_dims", "mcpx_module_unload", "mcpx_solve_batch_module", "mcpx_solve_batch_module_device",
-           "mcpx_host_register", "mcpx_host_unregister")
+           "mcpx_host_register", "mcpx_host_unregister", "mcpx_vjp_batch_module", "mcpx_vjp_batch_module_device",
+           "mcpx_jvp_batch_module", "mcpx_jvp_batch_module_device")
 
 
 def lib():
@@ -76,6 +77,15 @@ def lib():
     L.mcpx_solve_batch_module_device.restype = C.c_int
     L.mcpx_solve_batch_module_device.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P,
                                                  C.POINTER(_abi.Params), C.POINTER(_abi.Out), C.c_void_p]
+    L.mcpx_vjp_batch_module.restype = C.c_int
+    L.mcpx_vjp_batch_module.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P, P, P, P, C.c_int, P, P]
+    L.mcpx_vjp_batch_module_device.restype = C.c_int
+    L.mcpx_vjp_batch_module_device.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P, P, P, P, P, P, P]
+    L.mcpx_jvp_batch_module.restype = C.c_int
+    L.mcpx_jvp_batch_module.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, C.c_int, P, P]
+    L.mcpx_jvp_batch_module_device.restype = C.c_int
+    L.mcpx_jvp_batch_module_device.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, P, P,
+                                               P]
     L.mcpx_host_register.restype = C.c_int
     L.mcpx_host_register.argtypes = [C.c_void_p, C.c_size_t]
     L.mcpx_host_unregister.restype = C.c_int

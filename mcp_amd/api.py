@@ -420,7 +420,29 @@ class PrimalDualMCP:
                             sp.lambdify(args, sp.Matrix(GH).jacobian(zs), "numpy"))
         return self._nl_fns
 
+    def _nl_host_theta(self):
+        """Lambdified ∂(G; H)/∂θ of a nonlinear MCP (host inspection)."""
+        if getattr(self, "_nl_tfn", None) is None:
+            sp = _sp()
+            zs = list(self.x_symbolic) + list(self.y_symbolic)
+            args = zs + list(self.θ_symbolic)
+            GH = list(self.G_symbolic) + list(self.H_symbolic)
+            self._nl_tfn = sp.lambdify(args, sp.Matrix(GH).jacobian(list(self.θ_symbolic)), "numpy")
+        return self._nl_tfn
+
     # -- host evaluation of the reference callbacks (inspection / tests) ----
+    def jacobian_theta(self, x, y, s, *, θ, ϵ=None):
+        """∇F_θ (src/mcp.jl:122-147) of a nonlinear-family MCP as a dense N×p host array
+        (the s⊙y − ϵ rows are 0), w.r.t. the MCP's own parameters θ (host inspection; the
+        affine families' ∇F_θ is analytic, oracle/ipm_ref.py jacobian_theta)."""
+        if self.family != _abi.FAMILY_NONLINEAR:
+            raise TypeError("jacobian_theta is the nonlinear family's host check")
+        n, m, p = self.unconstrained_dimension, self.constrained_dimension, self.parameter_dimension
+        out = np.zeros((n + 2 * m, p))
+        x, y, th = (np.asarray(v, float) for v in (x, y, θ))
+        out[:n + m] = np.asarray(self._nl_host_theta()(*x, *y, *th), float).reshape(n + m, p)
+        return out
+
     def family_parameters(self, θ):
         """θ → θ' (the per-instance data the kernel reads), numpy or torch."""
         return self.theta_map(θ)

@@ -15,6 +15,11 @@ mcpx_vjp_* / mcpx_jvp_*).
   torch loss over (x, y, s) back-propagates into θ (the Zygote use of the
   reference's rrule, test/runtests.jl:65-85).
 
+Every family is covered: QP / affine through the analytic ∇F_θ of their θ
+layouts, nonlinear-family MCPs (the trajectory games of src/game.jl) through
+their generated module's ∇F_θ code; one wave per instance up to 64 KKT rows,
+one workgroup per instance beyond (include/mcpx.h).
+
 Where ∇F_z is exactly singular the kernels report it per instance
 (`status` 1) and return NaN; the reference's pivoted QR would return a basic
 least-squares solution there.
@@ -41,13 +46,16 @@ class NoTangent:
 
 
 def _require_sensitivities(mcp) -> None:
-    if getattr(mcp, "nl", None) is not None:
-        raise NotImplementedError("sensitivities of nonlinear-family MCPs (generated ∇F_θ code and a ≥ 90-dim "
-                                  "adjoint solve for the lane-change game) are not built yet (DESIGN.md §10)")
     # src/AutoDiff.jl:19-23
     if not getattr(mcp, "compute_sensitivities", False):
         raise ValueError("Missing sensitivities. Set `compute_sensitivities = True` when constructing the "
                          "PrimalDualMCP.")
+
+
+def _module(mcp):
+    """The generated module of a nonlinear-family MCP (its ∇F_θ is the generated
+    mcpx_nl_eval_theta, src/mcp.jl:122-147), else None (QP / affine kernels)."""
+    return mcp.module() if getattr(mcp, "nl", None) is not None else None
 
 
 def _is_torch(a) -> bool:
@@ -80,7 +88,7 @@ def solve_pullback(solution, dx=None, dy=None, ds=None, *, num_devices: int = 0,
         tp = mcp.theta_map(th).contiguous()
         f = lambda t: None if t is None else t.to(torch.float64).reshape(th.shape[0], -1).contiguous()
         dtp, st = vjp_batch_device(mcp.family, n, m, tp, f(solution.x), f(solution.y), f(solution.s),
-                                   f(dx), f(dy), f(ds))
+                                   f(dx), f(dy), f(ds), module=_module(mcp))
         dθ = mcp.theta_map.vjp(th, dtp)
         return (dθ, st) if return_status else dθ
     th = np.asarray(θ, dtype=np.float64)
@@ -90,21 +98,29 @@ def solve_pullback(solution, dx=None, dy=None, ds=None, *, num_devices: int = 0,
     tp = mcp.theta_map(th2)
     f = lambda a, k: None if a is None else np.asarray(a, np.float64).reshape(B, k)
     dtp, st = vjp_batch(mcp.family, n, m, tp, f(solution.x, n), f(solution.y, m), f(solution.s, m),
-                        f(dx, n), f(dy, m), f(ds, m), num_devices=num_devices)
+                        f(dx, n), f(dy, m), f(ds, m), num_devices=num_devices, module=_module(mcp))
     dθ = mcp.theta_map.vjp(th2, dtp)
     if single:
         dθ, st = dθ[0], st[0]
     return (dθ, st) if return_status else dθ
 
 
-def rrule(f, solver_type, mcp, θ, **kwargs):
+def rrule(f, solver_type, mcp, θ=None, **kwargs):
     """ChainRulesCore.rrule(solve, solver_type, mcp, θ; kwargs...) (src/AutoDiff.jl:42-82).
     Returns (solution, pullback); pullback(∂solution) → (NoTangent(), NoTangent(),
-    NoTangent(), ∂θ) where ∂solution has fields / keys x, y, s (missing = zero)."""
-    from .api import solve
+    NoTangent(), ∂θ) where ∂solution has fields / keys x, y, s (missing = zero).
+
+    rrule(solve, game, θ; kwargs...) differentiates a game solve (src/game.jl:196-212,
+    which calls solve(solver_type, game.mcp, θ) — the path Zygote takes through
+    examples/utils.jl:233-269): the solution is the GameSolution, ∂solution carries
+    `variables` (x, y, s) and/or `primals` (one block per player, added into ∂x);
+    pullback → (NoTangent(), NoTangent(), ∂θ)."""
+    from .api import ParametricGame, solve
 
     if f is not solve:
         raise TypeError("rrule is defined for mcp_amd.api.solve only")
+    if isinstance(solver_type, ParametricGame):
+        return _game_rrule(solver_type, mcp, **kwargs)
     _require_sensitivities(mcp)
     solution = solve(solver_type, mcp, θ, **kwargs)
 
@@ -113,6 +129,33 @@ def rrule(f, solver_type, mcp, θ, **kwargs):
         return NoTangent(), NoTangent(), NoTangent(), dθ
 
     return solution, solve_pullback_
+
+
+def _game_rrule(game, θ, solver_type=None, **kwargs):
+    from .api import GameSolution, InteriorPoint, solve
+
+    mcp = game.mcp
+    _require_sensitivities(mcp)
+    sol_mcp = solve(solver_type or InteriorPoint(), mcp, θ, **kwargs)  # src/game.jl:196-212
+    ends = np.cumsum(game.dims["x"])
+    starts = np.concatenate([[0], ends[:-1]])
+    x = sol_mcp.x
+    solution = GameSolution([x[..., a:b] for a, b in zip(starts, ends)],
+                            {"x": sol_mcp.x, "y": sol_mcp.y, "s": sol_mcp.s}, sol_mcp.kkt_error, sol_mcp.status)
+
+    def game_pullback(dsolution):
+        var = _get(dsolution, "variables") or {}
+        dx, dy, ds = _get(var, "x"), _get(var, "y"), _get(var, "s")
+        prim = _get(dsolution, "primals")
+        if prim is not None:  # ∂primals[i] is the cotangent of x[starts[i]:ends[i]]
+            acc = np.zeros(np.shape(x)) if dx is None else np.array(dx, np.float64)
+            for a, b, g in zip(starts, ends, prim):
+                if g is not None:
+                    acc[..., a:b] += np.asarray(g, np.float64)
+            dx = acc
+        return NoTangent(), NoTangent(), solve_pullback(sol_mcp, dx, dy, ds)
+
+    return solution, game_pullback
 
 
 @dataclass
@@ -153,7 +196,8 @@ def solve_dual(solver_type, mcp, θ, θ_partials, *, num_devices: int = 0, **kwa
     sol = solve(solver_type, mcp, th2, num_devices=num_devices, **kwargs)  # forward pass (:94)
     tp = mcp.theta_map(th2)
     tdot = mcp.theta_map.jvp(th2, np.ascontiguousarray(np.swapaxes(tpar, 1, 2)))  # (B, K, p')
-    zd, st = jvp_batch(mcp.family, n, m, tp, sol.x, sol.y, sol.s, tdot, num_devices=num_devices)  # (B, K, N)
+    zd, st = jvp_batch(mcp.family, n, m, tp, sol.x, sol.y, sol.s, tdot, num_devices=num_devices,
+                       module=_module(mcp))  # (B, K, N)
     zp = np.swapaxes(zd, 1, 2)  # (B, N, K): z_p = ∂z∂θ · θ_p (:98)
     xp, yp, sp_ = zp[:, :n], zp[:, n:n + m], zp[:, n + m:]
     pick = (lambda a: a[0]) if single else (lambda a: a)

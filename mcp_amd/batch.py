@@ -45,6 +45,14 @@ class Module:
         self.n, self.m, self.p, self.solvers = (x.value for x in v)
         self.path = path
 
+    @property
+    def has_vjp(self) -> bool:
+        return bool((self.solvers >> _abi.MODULE_VJP) & 1)
+
+    @property
+    def has_jvp(self) -> bool:
+        return bool((self.solvers >> _abi.MODULE_JVP) & 1)
+
     def close(self) -> None:
         if self.handle:
             lib().mcpx_module_unload(self.handle)
@@ -184,38 +192,52 @@ def _host_f64(a, shape):
     return None if a is None else np.ascontiguousarray(np.broadcast_to(a, shape), dtype=np.float64)
 
 
+def _pdim(family: int, n: int, m: int, module: Module | None) -> int:
+    return module.p if module is not None else _abi.theta_dim(family, n, m)
+
+
 def vjp_batch(family: int, n: int, m: int, theta, x, y, s, gx=None, gy=None, gs=None,
-              num_devices: int = 0) -> tuple:
+              num_devices: int = 0, module: Module | None = None) -> tuple:
     """rrule pullback on the GPU(s) for host arrays: ∂θ = (∂z/∂θ)ᵀ [gx; gy; gs]
     (src/AutoDiff.jl:59-76).  None cotangents are zero.  Returns
-    (dtheta (B, p) in the family's θ layout, status (B,) int32: 1 = ∇F_z singular)."""
+    (dtheta (B, p) in the family's θ layout, status (B,) int32: 1 = ∇F_z singular).
+    `module`: the generated module of a nonlinear-family MCP (mcpx_vjp_batch_module)."""
     theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
     B, ld = theta.shape
-    p = _abi.theta_dim(family, n, m)
+    p = _pdim(family, n, m, module)
     x, y, s = _host_f64(x, (B, n)), _host_f64(y, (B, m)), _host_f64(s, (B, m))
     gx, gy, gs = _host_f64(gx, (B, n)), _host_f64(gy, (B, m)), _host_f64(gs, (B, m))
     dth = np.empty((B, p))
     st = np.empty(B, np.int32)
     desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
-    check(lib().mcpx_vjp_batch(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), _ptr(gx), _ptr(gy),
-                               _ptr(gs), int(num_devices), _ptr(dth), _ptr(st)))
+    if module is not None:
+        check(lib().mcpx_vjp_batch_module(module.handle, C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s),
+                                          _ptr(gx), _ptr(gy), _ptr(gs), int(num_devices), _ptr(dth), _ptr(st)))
+    else:
+        check(lib().mcpx_vjp_batch(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), _ptr(gx), _ptr(gy),
+                                   _ptr(gs), int(num_devices), _ptr(dth), _ptr(st)))
     return dth, st
 
 
-def jvp_batch(family: int, n: int, m: int, theta, x, y, s, theta_dot, num_devices: int = 0) -> tuple:
+def jvp_batch(family: int, n: int, m: int, theta, x, y, s, theta_dot, num_devices: int = 0,
+              module: Module | None = None) -> tuple:
     """ForwardDiff-Dual tangents on the GPU(s): ż = (∂z/∂θ) θ̇ (src/AutoDiff.jl:94-100).
     theta_dot (B, K, p) → (zdot (B, K, n+2m), status (B,))."""
     theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
     B, ld = theta.shape
-    p = _abi.theta_dim(family, n, m)
+    p = _pdim(family, n, m, module)
     td = np.ascontiguousarray(theta_dot, dtype=np.float64).reshape(B, -1, p)
     K = td.shape[1]
     x, y, s = _host_f64(x, (B, n)), _host_f64(y, (B, m)), _host_f64(s, (B, m))
     zd = np.empty((B, K, n + 2 * m))
     st = np.empty(B, np.int32)
     desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
-    check(lib().mcpx_jvp_batch(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), int(K), _ptr(td),
-                               int(num_devices), _ptr(zd), _ptr(st)))
+    if module is not None:
+        check(lib().mcpx_jvp_batch_module(module.handle, C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s),
+                                          int(K), _ptr(td), int(num_devices), _ptr(zd), _ptr(st)))
+    else:
+        check(lib().mcpx_jvp_batch(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), int(K), _ptr(td),
+                                   int(num_devices), _ptr(zd), _ptr(st)))
     return zd, st
 
 
@@ -230,7 +252,7 @@ def _dev_f64(t, what):
 
 
 def vjp_batch_device(family: int, n: int, m: int, theta, x, y, s, gx=None, gy=None, gs=None, dtheta=None,
-                     status=None, stream=None):
+                     status=None, stream=None, module: Module | None = None):
     """Device-tensor pullback enqueued on the current stream (no sync).
     Returns (dtheta (B, p), status (B,) int32) tensors."""
     import torch
@@ -238,7 +260,7 @@ def vjp_batch_device(family: int, n: int, m: int, theta, x, y, s, gx=None, gy=No
     if not (theta.is_cuda and theta.dtype == torch.float64 and theta.dim() == 2 and theta.is_contiguous()):
         raise ValueError("theta must be a contiguous (B, p) float64 device tensor")
     B, ld = theta.shape
-    p = _abi.theta_dim(family, n, m)
+    p = _pdim(family, n, m, module)
     dev = theta.device
     if dtheta is None:
         dtheta = torch.empty(B, p, dtype=torch.float64, device=dev)
@@ -247,20 +269,25 @@ def vjp_batch_device(family: int, n: int, m: int, theta, x, y, s, gx=None, gy=No
     ptrs = [_dev_f64(t, k) for t, k in ((x, "x"), (y, "y"), (s, "s"), (gx, "gx"), (gy, "gy"), (gs, "gs"))]
     desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
     st = stream if stream is not None else torch.cuda.current_stream(dev)
-    check(lib().mcpx_vjp_batch_device(C.byref(desc), theta.data_ptr(), *ptrs, _dev_f64(dtheta, "dtheta"),
-                                      status.data_ptr(), C.c_void_p(st.cuda_stream)))
+    if module is not None:
+        check(lib().mcpx_vjp_batch_module_device(module.handle, C.byref(desc), theta.data_ptr(), *ptrs,
+                                                 _dev_f64(dtheta, "dtheta"), status.data_ptr(),
+                                                 C.c_void_p(st.cuda_stream)))
+    else:
+        check(lib().mcpx_vjp_batch_device(C.byref(desc), theta.data_ptr(), *ptrs, _dev_f64(dtheta, "dtheta"),
+                                          status.data_ptr(), C.c_void_p(st.cuda_stream)))
     return dtheta, status
 
 
 def jvp_batch_device(family: int, n: int, m: int, theta, x, y, s, theta_dot, zdot=None, status=None,
-                     stream=None):
+                     stream=None, module: Module | None = None):
     """Device-tensor tangents: theta_dot (B, K, p) → (zdot (B, K, n+2m), status (B,))."""
     import torch
 
     if not (theta.is_cuda and theta.dtype == torch.float64 and theta.dim() == 2 and theta.is_contiguous()):
         raise ValueError("theta must be a contiguous (B, p) float64 device tensor")
     B, ld = theta.shape
-    p = _abi.theta_dim(family, n, m)
+    p = _pdim(family, n, m, module)
     td = theta_dot.reshape(B, -1, p)
     K = td.shape[1]
     dev = theta.device
@@ -270,7 +297,9 @@ def jvp_batch_device(family: int, n: int, m: int, theta, x, y, s, theta_dot, zdo
         status = torch.empty(B, dtype=torch.int32, device=dev)
     desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
     st = stream if stream is not None else torch.cuda.current_stream(dev)
-    check(lib().mcpx_jvp_batch_device(C.byref(desc), theta.data_ptr(), _dev_f64(x, "x"), _dev_f64(y, "y"),
-                                      _dev_f64(s, "s"), int(K), _dev_f64(td.contiguous(), "theta_dot"),
-                                      _dev_f64(zdot, "zdot"), status.data_ptr(), C.c_void_p(st.cuda_stream)))
+    fn = lib().mcpx_jvp_batch_device if module is None else (
+        lambda *a: lib().mcpx_jvp_batch_module_device(module.handle, *a))
+    check(fn(C.byref(desc), theta.data_ptr(), _dev_f64(x, "x"), _dev_f64(y, "y"), _dev_f64(s, "s"), int(K),
+             _dev_f64(td.contiguous(), "theta_dot"), _dev_f64(zdot, "zdot"), status.data_ptr(),
+             C.c_void_p(st.cuda_stream)))
     return zdot, status

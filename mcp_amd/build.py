@@ -26,9 +26,9 @@ LIB = os.path.join(HERE, "libmcpx.so")
 SOURCES = [os.path.join(CSRC, f) for f in (
     "ipm_inst_red_qp.hip", "ipm_inst_spec.hip", "ipm_inst_schur_qp.hip", "ipm_inst_red_aff.hip",
     "ipm_inst_dense_qp.hip", "ipm_inst_dense_aff.hip", "sens_inst_vjp.hip", "sens_inst_jvp.hip",
-    "ipm_inst_wg.hip", "mcpx_api.cpp")]
+    "ipm_inst_wg.hip", "sens_inst_wg.hip", "mcpx_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("ipm_kernel.h", "ipm_kernel_impl.hpp", "bcast_group.inc", "sens_kernel.h", "sens_kernel_impl.hpp",
-    "ipm_wg.h", "ipm_wg_impl.hpp")] + [
+    "ipm_wg.h", "ipm_wg_impl.hpp", "sens_wg_impl.hpp")] + [
     os.path.join(ROOT, "include", "mcpx.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
@@ -91,7 +91,13 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     # hipcc does not pad hazards whose reader sits inside inline asm: refuse a build in
     # which a compiler-placed VALU write feeds a DPP / cross-lane asm read too early
     checker = os.path.join(ROOT, "tools", "check_dpp_hazards.py")
-    for asm in sorted(glob.glob(os.path.join(tmp_dir, "*amdgcn*gfx950.s"))):
+    asms = sorted(glob.glob(os.path.join(tmp_dir, "*amdgcn*gfx950.s")))
+    if not os.path.exists(checker):
+        raise RuntimeError(f"the inline-asm hazard checker {checker} is missing: refusing an unchecked build")
+    if len(asms) < sum(1 for s in SOURCES if s.endswith(".hip")):  # every kernel TU leaves its device .s
+        raise RuntimeError(f"found {len(asms)} device .s files under {tmp_dir} for the hazard check "
+                           "(-save-temps naming changed?): refusing an unchecked build")
+    for asm in asms:
         r = subprocess.run([sys.executable, checker, asm], capture_output=True, text=True)
         if verbose:
             print(f"{os.path.basename(asm)}: {r.stdout.strip().splitlines()[-1]}", flush=True)

@@ -20,7 +20,18 @@ and tables (MCPX_NL_TABLE: `__constant__` on the GPU, `static const` in C):
                              z = [x; y], once per Newton step;
   mcpx_nl_qk_ptr / _idx      K(i): the structural nonzeros of row i of Q;
   mcpx_nl_rj_ptr / _idx      J(k): the structural nonzeros of row k of R
-                             (the SCHUR elimination's sparse terms).
+                             (the SCHUR elimination's sparse terms);
+  mcpx_nl_eval_theta(th, z, dth)  ∇F_θ at z = [x; y] — the reference's ∇F_θ!
+                             (src/mcp.jl:122-147), used by the sensitivity
+                             kernels (src/AutoDiff.jl:18-40): the G and H rows
+                             (the s⊙y − ϵ rows do not depend on θ) as an
+                             (n+m)×p column-major block, dth[t·(n+m) + i] =
+                             ∂[G; H]_i/∂θ_t, structural nonzeros only;
+  mcpx_nl_tc_ptr / _idx      rows of column t of ∇F_θ with a structural
+                             nonzero (CSR by θ column, ascending): the pullback
+                             ∂θ_t = −Σ_i ∇F_θ[i, t] λ_i takes exactly these terms;
+  mcpx_nl_tr_ptr / _idx      θ columns of row i (CSR by row, ascending): the
+                             tangent (∇F_θ θ̇)_i of the JVP.
 
 Block layout of `blk` (doubles, column-major blocks like the affine family):
 
@@ -62,11 +73,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 Z_VOLATILE_ABOVE = int(os.environ.get("MCPX_NL_Z_VOLATILE_ABOVE", "128"))
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
-GEN_VERSION = 4
+GEN_VERSION = 5
 _MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function",
                  "-mllvm", "-amdgpu-mfma-vgpr-form=1")
 _MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "ipm_wg.h",
-                "ipm_wg_impl.hpp", "../../include/mcpx.h")
+                "ipm_wg_impl.hpp", "sens_wg_impl.hpp", "sens_kernel.h", "../../include/mcpx.h")
 WG_LDS_LIMIT = 160 * 1024 - 2048  # MCPX_NL_WG_LIMIT of csrc/ipm_nl_kernel.hpp
 LDS_LIMIT = 160 * 1024 - 2048  # bytes of static LDS one workgroup may declare on gfx950 (minus headroom)
 
@@ -207,6 +218,12 @@ class NLSystem:
         self.residuals = ([(self.OFF_G + i, g) for i, g in enumerate(self.G)]
                           + [(self.OFF_H + k, h) for k, h in enumerate(self.H)])
         self.nnz = len(self.const_entries) + len(self.var_entries)
+        # ∇F_θ of the G and H rows (src/mcp.jl:122-147), dth[t·(n+m) + i]
+        nr = n + m
+        self.theta_entries = sorted(
+            [(t * nr + i, d) for i, e in enumerate(self.G + self.H) for t, th in enumerate(self.ts)
+             if (d := sp.diff(e, th)) != 0], key=lambda t: t[0])
+        self.nnz_theta = len(self.theta_entries)
         self.body = self._emit()
         self.key = hashlib.sha256(f"v{GEN_VERSION}\n{self.body}".encode()).hexdigest()[:24]
 
@@ -245,7 +262,7 @@ class NLSystem:
         raise NotImplementedError(f"nonlinear MCP with n={self.n}, m={self.m} exceeds every kernel's LDS budget")
 
     # ---- emission ------------------------------------------------------------
-    def _block(self, entries, with_z: bool) -> list:
+    def _block(self, entries, with_z: bool, out: str = "blk") -> list:
         """Straight-line C for `entries` after common-subexpression elimination.  Each
         CSE temporary is emitted right before the first statement that needs it
         (dependency order kept), not all at the top: at horizon T = 10 the
@@ -278,7 +295,7 @@ class NLSystem:
                 lines.append(f"  const double {sym} = {pr(rep_of[sym])};")
                 names[sym] = str(sym)
                 emitted.add(sym)
-            lines.append(f"  blk[{idx}] = {pr(e)};")
+            lines.append(f"  {out}[{idx}] = {pr(e)};")
         return lines
 
     def structure(self):
@@ -295,10 +312,23 @@ class NLSystem:
                             [x for r in rows for x in r])
         return csr(qk), csr(rj)
 
+    def theta_structure(self):
+        """Structural nonzeros of ∇F_θ's G/H rows: (ptr, idx) CSR by θ column (rows i
+        ascending) and by row (θ columns t ascending)."""
+        nr, p = self.n + self.m, self.p
+        ents = [idx for idx, _ in self.theta_entries]
+        cols = [[idx - t * nr for idx in ents if idx // nr == t] for t in range(p)]
+        rows = [[idx // nr for idx in ents if idx % nr == i] for i in range(nr)]
+        acc = __import__("itertools").accumulate
+        csr = lambda rr: ([0] + list(acc(len(r) for r in rr)), [x for r in rr for x in r])
+        return csr(cols), csr(rows)
+
     def _emit(self) -> str:
         init = self._block(self.const_entries, with_z=False)
         ev = self._block(self.var_entries + self.residuals, with_z=True)
+        evt = self._block(self.theta_entries, with_z=True, out="dth")
         (qp, qi), (rp, ri) = self.structure()
+        (tcp, tci), (trp, tri) = self.theta_structure()
         arr = lambda name, v: f"MCPX_NL_TABLE int32_t {name}[{max(len(v), 1)}] = {{{', '.join(map(str, v)) or '0'}}};"
         return "\n".join([
             "/* generated by mcp_amd/codegen.py — do not edit */",
@@ -310,11 +340,17 @@ class NLSystem:
             f"#define MCPX_NL_NNZ {self.nnz}",
             f"#define MCPX_NL_NNZ_Q {len(qi)}",
             f"#define MCPX_NL_NNZ_R {len(ri)}",
+            f"#define MCPX_NL_NNZ_T {self.nnz_theta}",
             "/* structural nonzeros: K(i) of Q row i, J(k) of R row k (CSR, ascending) */",
             arr("mcpx_nl_qk_ptr", qp),
             arr("mcpx_nl_qk_idx", qi),
             arr("mcpx_nl_rj_ptr", rp),
             arr("mcpx_nl_rj_idx", ri),
+            "/* structural nonzeros of ∇F_θ (G/H rows): rows of column t, columns of row i (CSR) */",
+            arr("mcpx_nl_tc_ptr", tcp),
+            arr("mcpx_nl_tc_idx", tci),
+            arr("mcpx_nl_tr_ptr", trp),
+            arr("mcpx_nl_tr_idx", tri),
             "MCPX_NL_FN void mcpx_nl_init(const double* MCPX_NL_RESTRICT th, double* MCPX_NL_RESTRICT blk) {",
             "  (void)th;",
             "  (void)blk;",
@@ -325,6 +361,13 @@ class NLSystem:
             "  (void)th;",
             "  (void)z;",
             *ev,
+            "}",
+            "MCPX_NL_FN void mcpx_nl_eval_theta(const double* MCPX_NL_RESTRICT th, const double* MCPX_NL_RESTRICT z,",
+            "                                   double* MCPX_NL_RESTRICT dth) {",
+            "  (void)th;",
+            "  (void)z;",
+            "  (void)dth;",
+            *evt,
             "}",
             "",
         ])
@@ -388,8 +431,11 @@ def _check_hazards(tmp_dir: str) -> None:
     """The inline-asm hazard check of the main build (mcp_amd/build.py) on the module's ISA."""
     checker = os.path.join(os.path.dirname(HERE), "tools", "check_dpp_hazards.py")
     if not os.path.exists(checker):
-        return
-    for asm in glob.glob(os.path.join(tmp_dir, "*gfx950*.s")):
+        raise RuntimeError(f"the inline-asm hazard checker {checker} is missing: refusing an unchecked module")
+    asms = glob.glob(os.path.join(tmp_dir, "*gfx950*.s"))
+    if not asms:
+        raise RuntimeError(f"no device .s under {tmp_dir} for the hazard check (-save-temps naming changed?)")
+    for asm in asms:
         r = subprocess.run([sys.executable, checker, asm], capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"inline-asm hazard in the generated module:\n{r.stdout[-2000:]}")

@@ -412,7 +412,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
 #define MCPX_NL_CAN_WG_DENSE (MCPX_NL_NV >= 1 && MCPX_NL_WG_LDS(MCPX_NL_NV) <= MCPX_NL_WG_LIMIT)
 #define MCPX_NL_CAN_WG_SCHUR (!MCPX_NL_HAS_S && MCPX_NL_N >= 1 && MCPX_NL_WG_LDS(MCPX_NL_N) <= MCPX_NL_WG_LIMIT)
 
-#include "ipm_wg_impl.hpp"
+#include "sens_wg_impl.hpp"
 
 namespace mcpx {
 namespace nl {
@@ -427,20 +427,40 @@ struct Gen {
   __device__ static const int32_t* qk_idx() { return mcpx_nl_qk_idx; }
   __device__ static const int32_t* rj_ptr() { return mcpx_nl_rj_ptr; }
   __device__ static const int32_t* rj_idx() { return mcpx_nl_rj_idx; }
+  __device__ static void eval_theta(const double* th, const double* z, double* dth) { mcpx_nl_eval_theta(th, z, dth); }
+  __device__ static const int32_t* tc_ptr() { return mcpx_nl_tc_ptr; }
+  __device__ static const int32_t* tc_idx() { return mcpx_nl_tc_idx; }
+  __device__ static const int32_t* tr_ptr() { return mcpx_nl_tr_ptr; }
+  __device__ static const int32_t* tr_idx() { return mcpx_nl_tr_idx; }
 };
 constexpr int NVW = imax(1, N);
 }  // namespace nl
 }  // namespace mcpx
 
-// mcpx_nl_meta: {layout version, n, m, p, has_s, kernel mask, block size, nnz}; kernel
-// mask: bit MCPX_LINSOLVE_* = one-wave kernel, bit 3 + MCPX_LINSOLVE_* = workgroup kernel
+// mcpx_nl_meta: {layout version, n, m, p, has_s, kernel mask, block size, nnz, nnz of ∇F_θ,
+// 0, 0, 0}; kernel mask: bit MCPX_LINSOLVE_* = one-wave kernel, bit 3 + MCPX_LINSOLVE_* =
+// workgroup kernel, bit MCPX_MODULE_VJP / MCPX_MODULE_JVP = sensitivity kernels (the
+// VJP factors the (n+m)-dim system of the REDUCED workgroup solver, the JVP the full
+// (n+2m)-dim ∇F_z of the DENSE one: they exist when those fit LDS)
 extern "C" {
-__device__ int32_t mcpx_nl_meta[8] = {
-    2, MCPX_NL_N, MCPX_NL_M, MCPX_NL_P, MCPX_NL_HAS_S,
+__device__ int32_t mcpx_nl_meta[12] = {
+    3, MCPX_NL_N, MCPX_NL_M, MCPX_NL_P, MCPX_NL_HAS_S,
     (MCPX_NL_CAN_REDUCED << MCPX_LINSOLVE_REDUCED) | (MCPX_NL_CAN_DENSE << MCPX_LINSOLVE_DENSE) |
         (MCPX_NL_CAN_SCHUR << MCPX_LINSOLVE_SCHUR) | (MCPX_NL_CAN_WG_REDUCED << (3 + MCPX_LINSOLVE_REDUCED)) |
-        (MCPX_NL_CAN_WG_DENSE << (3 + MCPX_LINSOLVE_DENSE)) | (MCPX_NL_CAN_WG_SCHUR << (3 + MCPX_LINSOLVE_SCHUR)),
-    MCPX_NL_SIZE, MCPX_NL_NNZ};
+        (MCPX_NL_CAN_WG_DENSE << (3 + MCPX_LINSOLVE_DENSE)) | (MCPX_NL_CAN_WG_SCHUR << (3 + MCPX_LINSOLVE_SCHUR)) |
+        (MCPX_NL_CAN_WG_REDUCED << MCPX_MODULE_VJP) | (MCPX_NL_CAN_WG_DENSE << MCPX_MODULE_JVP),
+    MCPX_NL_SIZE, MCPX_NL_NNZ, MCPX_NL_NNZ_T, 0, 0, 0};
+
+#if MCPX_NL_CAN_WG_REDUCED
+__global__ __launch_bounds__(256) void mcpx_nl_vjp_wg(const mcpx::wg::WgSensArgs args) {
+  mcpx::wg::sens_instances<MCPX_FAMILY_NONLINEAR, false, mcpx::nl::NVW, MCPX_NL_N + MCPX_NL_M, mcpx::nl::Gen>(args);
+}
+#endif
+#if MCPX_NL_CAN_WG_DENSE
+__global__ __launch_bounds__(256) void mcpx_nl_jvp_wg(const mcpx::wg::WgSensArgs args) {
+  mcpx::wg::sens_instances<MCPX_FAMILY_NONLINEAR, true, mcpx::nl::NVW, mcpx::nl::NVW, mcpx::nl::Gen>(args);
+}
+#endif
 
 #if MCPX_NL_CAN_WG_REDUCED
 __global__ __launch_bounds__(256) void mcpx_nl_solve_reduced_wg(const mcpx::wg::WgArgs args) {

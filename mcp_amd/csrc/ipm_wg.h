@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "ipm_kernel.h"
+#include "sens_kernel.h"
 
 namespace mcpx {
 namespace wg {
@@ -25,6 +26,24 @@ struct WgArgs {
   int32_t pad_;
 };
 
+// Sensitivity kernels of the workgroup-per-instance layout (sens_wg_impl.hpp): the
+// one-wave SensArgs plus the work queue and the per-slot workspace — [K | rhs] of the
+// slack-eliminated (n+m)-dim ∇F_zᵀ system (VJP) or of the full (n+2m)-dim ∇F_z (JVP,
+// `nrhs` partials per factorisation), and for a generated module its Jacobian blocks
+// and ∇F_θ.
+struct WgSensArgs {
+  SensArgs s;
+  double* work;         // grid slots × slot_stride doubles
+  int32_t* counter;     // work-queue head, zeroed before the launch
+  int64_t batch;        // instances
+  int64_t slot_stride;  // doubles per slot
+  int64_t off_blk;      // nonlinear family: generated Jacobian blocks (MCPX_NL_SIZE doubles)
+  int64_t off_dth;      // nonlinear family: ∇F_θ of the G/H rows, (n+m) × p column-major
+  int64_t off_sol;      // JVP: the nrhs solutions (nrhs × ns)
+  int32_t ld;           // row stride of [K | rhs] (≥ ns + nrhs)
+  int32_t nrhs;         // right-hand sides per factorisation (JVP partials; 1 for the VJP)
+};
+
 constexpr int kThreads = 256;       // workgroup size of every workgroup kernel
 constexpr int kMaxDim = 768;        // largest system / vector dimension of the QP / affine kernels
 constexpr int kDimBuckets[4] = {128, 256, 512, 768};
@@ -36,5 +55,10 @@ constexpr int kDimBuckets[4] = {128, 256, 512, 768};
 // and the launch; hipErrorInvalidValue when no such kernel exists.
 const void* ipm_wg_kernel(int family, int solver, int nv);
 hipError_t launch_ipm_wg(int family, int solver, int nv, const wg::WgArgs& a, int grid, hipStream_t st);
+// Sensitivity kernels of the QP and affine families beyond the one-wave kernels'
+// 64 rows (sens_inst_wg.hip): VJP (jvp = false) or JVP at vector dimension
+// n + 2m ≤ nv ∈ wg::kDimBuckets.
+const void* sens_wg_kernel(int family, bool jvp, int nv);
+hipError_t launch_sens_wg(int family, bool jvp, int nv, const wg::WgSensArgs& a, int grid, hipStream_t st);
 
 }  // namespace mcpx

@@ -132,8 +132,11 @@ __device__ __forceinline__ uint64_t pivot_key(double a) {
 
 // ---- blocked LU with partial pivoting (oracle lu_solve) --------------------
 //
-// A: ns × (ns + 1) row-major with stride ld, column ns = rhs; destroyed.
-// x (LDS, ≥ ns): the solution, x[k] = δz_k.
+// A: ns × (ns + nrhs) row-major with stride ld, columns ns .. ns+nrhs−1 = right-hand
+// sides (each sees exactly the oracle's single-rhs chain: they are trailing columns of the
+// same elimination); destroyed.  x (LDS, ≥ ns): the solution of the last right-hand side,
+// x[k] = δz_k; with xout, the solution of right-hand side c is also stored at
+// xout[c·ns + k] (the sensitivity kernels' several partials).
 template <int NSMAX>
 struct LuShared {
   double pan[NSMAX * NB];     // the panel, row q = remaining-list position q
@@ -178,7 +181,8 @@ __device__ __forceinline__ int panel_pivot(LuShared<NSMAX>& L, int r, int kk, in
 }
 
 template <int NSMAX>
-__device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuShared<NSMAX>& L) {
+__device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuShared<NSMAX>& L,
+                                         int nrhs = 1, double* __restrict__ xout = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < ns; i += WG) L.rem[i] = (int16_t)i;
   int r = ns;  // remaining rows (list length)
@@ -222,8 +226,9 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
         if (kk < kb) dst[kk] = L.pan[q * NB + kk];
     }
     // ---- U12: in-panel forward substitution of the pivot rows' trailing part -
-    const int j_lo = k0 + kb;  // trailing columns j_lo .. ns (rhs = column ns)
-    for (int j = j_lo + tid; j <= ns; j += WG) {
+    const int j_lo = k0 + kb;  // trailing columns j_lo .. ns+nrhs−1 (right-hand sides from column ns)
+    const int jend = ns + nrhs;
+    for (int j = j_lo + tid; j < jend; j += WG) {
       double u[NB];
 #pragma unroll
       for (int kk = 0; kk < NB; ++kk) {
@@ -239,7 +244,7 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
     }
     __syncthreads();
     // ---- trailing update of the other remaining rows on the matrix cores -----
-    const int ncol = ns + 1 - j_lo;
+    const int ncol = jend - j_lo;
     if (ncol > 0 && r > kb) {
       const int rt = (r + 15) / 16, ct = (ncol + 15) / 16;
       const int lr = lane >> 4, lc = lane & 15;
@@ -248,7 +253,7 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
       for (int t = wave; t < rt * ct; t += NWAVE) {
         const int ti = t / ct, tj = t - ti * ct;
         const int j = j_lo + 16 * tj + lc;
-        const bool jin = j <= ns;
+        const bool jin = j < jend;
         d4 acc;
         int64_t rowo[4];
         bool rin[4];
@@ -330,10 +335,15 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
 #pragma unroll
   for (int q = 0; q < RPT; ++q) {
     const int i = q * WG + tid;
-    b[q] = i < ns ? A[(int64_t)i * ld + ns] : 0.0;
     st[q] = i < ns ? L.step_of[i] : 0x7fff;
   }
   const int nblk = (ns + NB - 1) / NB;
+  for (int rc = 0; rc < nrhs; ++rc) {  // one back substitution per right-hand side
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
+    const int i = q * WG + tid;
+    b[q] = i < ns ? A[(int64_t)i * ld + ns + rc] : 0.0;
+  }
   for (int blk = nblk - 1; blk >= 0; --blk) {
     const int k0 = blk * NB, kb = min(NB, ns - k0);
     // the block's pivot rows publish their rhs (final but for the block's own terms)
@@ -370,6 +380,11 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
     }
   }
   __syncthreads();
+  if (xout) {
+    for (int k = tid; k < ns; k += WG) xout[(int64_t)rc * ns + k] = x[k];
+    __syncthreads();
+  }
+  }  // right-hand side c
   return true;
 }
 
@@ -381,6 +396,11 @@ struct NoGen {
   static constexpr bool HAS_S = false;
   __device__ static void init(const double*, double*) {}
   __device__ static void eval(const double*, const double*, double*) {}
+  __device__ static void eval_theta(const double*, const double*, double*) {}
+  __device__ static const int32_t* tc_ptr() { return nullptr; }
+  __device__ static const int32_t* tc_idx() { return nullptr; }
+  __device__ static const int32_t* tr_ptr() { return nullptr; }
+  __device__ static const int32_t* tr_idx() { return nullptr; }
   __device__ static const int32_t* qk_ptr() { return nullptr; }
   __device__ static const int32_t* qk_idx() { return nullptr; }
   __device__ static const int32_t* rj_ptr() { return nullptr; }

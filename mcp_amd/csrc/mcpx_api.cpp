@@ -30,7 +30,7 @@
 // code object image, its metadata record and the per-device loaded modules.
 struct mcpx_module {
   std::vector<char> image;
-  int32_t meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // mcpx_nl_meta of csrc/ipm_nl_kernel.hpp
+  int32_t meta[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // mcpx_nl_meta of csrc/ipm_nl_kernel.hpp
   std::mutex mu;
   std::map<int, hipModule_t> loaded;  // device → module, loaded on first use
 };
@@ -177,7 +177,7 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
 }
 
 // ---- generated nonlinear modules ---------------------------------------------
-constexpr int32_t kNLLayout = 2;  // mcpx_nl_meta[0] of csrc/ipm_nl_kernel.hpp
+constexpr int32_t kNLLayout = 3;  // mcpx_nl_meta[0] of csrc/ipm_nl_kernel.hpp
 const char* const kNLKernel[3] = {"mcpx_nl_solve_reduced", "mcpx_nl_solve_dense", "mcpx_nl_solve_schur"};
 
 // `mod` on device `dev` (the current device), loaded on first use.
@@ -246,6 +246,8 @@ void set_chunk(mcpx::KernelArgs& a, const mcpx_desc* d, const double* theta, con
   a.trace_len = o->alpha_trace ? o->trace_len : 0;
 }
 
+hipError_t pool_malloc(void** p, size_t bytes, hipStream_t st);  // the library's own pool (below)
+
 // Workgroup-per-instance launch (ipm_wg_impl.hpp): a persistent grid of the
 // resident workgroups pulls instances from an atomic counter; each workgroup
 // slot owns a workspace in HBM ([K | rhs] row-major, and for a generated module
@@ -281,7 +283,7 @@ int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const d
   const int64_t grid_max = std::min(slots_max, std::min(CH, d->batch));
   double* ws = nullptr;
   const size_t bytes = sizeof(double) * (size_t)(grid_max * w.slot_stride) + 256;
-  HIP_TRY(hipMallocAsync((void**)&ws, bytes, st));
+  HIP_TRY(pool_malloc((void**)&ws, bytes, st));
   w.work = ws;
   w.counter = (int32_t*)(ws + grid_max * w.slot_stride);
   int rc = MCPX_OK;
@@ -341,21 +343,45 @@ struct DevBuf {
   hipError_t alloc(size_t count) { return count ? hipMalloc(&p, count * sizeof(T)) : hipSuccess; }
 };
 
-// Device allocations of the host-buffer path come from the device's default
-// stream-ordered pool, kept warm across calls: the first call per device raises the
-// pool's release threshold, so freed blocks are reused by the next call instead of
-// returning to the driver (the caching a long-lived handle would give).
-int keep_pool_warm(int dev) {
+// Device allocations of the host-buffer path and the workgroup kernels' workspaces come
+// from the library's own stream-ordered pool per device (hipMemPoolCreate).  Freed blocks
+// stay in it for the next call up to kPoolKeep bytes (its release threshold: the caching a
+// long-lived handle would give, bounded), and the device's default pool — shared with torch
+// and every other allocator in the process — keeps its own attributes.  The pools live for
+// the process (no HIP calls during teardown).
+constexpr uint64_t kPoolKeep = 4ull << 30;
+
+int lib_pool(int dev, hipMemPool_t* out) {
   static std::mutex mu;
-  static std::map<int, bool> done;
+  static std::map<int, hipMemPool_t> pools;
   std::lock_guard<std::mutex> lock(mu);
-  if (done[dev]) return MCPX_OK;
+  auto it = pools.find(dev);
+  if (it != pools.end()) {
+    *out = it->second;
+    return MCPX_OK;
+  }
+  hipMemPoolProps props;
+  std::memset(&props, 0, sizeof props);
+  props.allocType = hipMemAllocationTypePinned;
+  props.location.type = hipMemLocationTypeDevice;
+  props.location.id = dev;
   hipMemPool_t pool;
-  HIP_TRY(hipDeviceGetDefaultMemPool(&pool, dev));
-  uint64_t keep = UINT64_MAX;
+  HIP_TRY(hipMemPoolCreate(&pool, &props));
+  uint64_t keep = kPoolKeep;
   HIP_TRY(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
-  done[dev] = true;
+  pools[dev] = pool;
+  *out = pool;
   return MCPX_OK;
+}
+
+// Stream-ordered allocation from the library pool of the current device.
+hipError_t pool_malloc(void** p, size_t bytes, hipStream_t st) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipMemPool_t pool;
+  if (lib_pool(dev, &pool) != MCPX_OK) return hipErrorOutOfMemory;
+  return hipMallocFromPoolAsync(p, bytes, pool, st);
 }
 
 template <class T>
@@ -364,7 +390,7 @@ struct AsyncBuf {  // stream-ordered device buffer, freed on the stream it was a
   hipStream_t st = nullptr;
   hipError_t alloc(size_t count, hipStream_t s) {
     st = s;
-    return count ? hipMallocAsync((void**)&p, count * sizeof(T), s) : hipSuccess;
+    return count ? pool_malloc((void**)&p, count * sizeof(T), s) : hipSuccess;
   }
   ~AsyncBuf() { if (p) (void)hipFreeAsync(p, st); }
 };
@@ -404,6 +430,14 @@ struct Pipe {
     }
     return hipSuccess;
   }
+  void destroy() {  // a Pipe whose init() failed part-way: release what it created
+    for (int k = 0; k < kMaxHostBufs; ++k) {
+      if (copied[k]) (void)hipEventDestroy(copied[k]);
+      if (consumed[k]) (void)hipEventDestroy(consumed[k]);
+    }
+    if (up) (void)hipStreamDestroy(up);
+    if (comp) (void)hipStreamDestroy(comp);
+  }
 };
 
 std::mutex g_pipe_mu;
@@ -424,7 +458,11 @@ struct PipeLease {  // a Pipe of device `dev` for the duration of one call (curr
       }
     }
     Pipe* q = new Pipe;
-    if (hipError_t e = q->init(); e != hipSuccess) return fail(MCPX_EHIP, "stream setup: %s", hipGetErrorString(e));
+    if (hipError_t e = q->init(); e != hipSuccess) {
+      q->destroy();
+      delete q;
+      return fail(MCPX_EHIP, "stream setup: %s", hipGetErrorString(e));
+    }
     p = q;
     return MCPX_OK;
   }
@@ -453,7 +491,6 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   if ((rc = prepare(d, prm, &a, &nmax, mod, &wg))) return rc;
   const int n = d->n, m = d->m;
   if (m > 64 && o->active_mask) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
-  if ((rc = keep_pool_warm(dev))) return rc;
   PipeLease lease;
   if ((rc = lease.acquire(dev))) return rc;
   Pipe* P = lease.p;
@@ -466,6 +503,15 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   AsyncBuf<int32_t> outer, status, newton;
   AsyncBuf<uint64_t> am;
   AsyncBuf<uint8_t> tr;
+  // declared after the buffers, so it runs before their (stream-ordered) frees on every
+  // exit: no upload or kernel may still target a buffer when it returns to the pool
+  struct Drain {
+    hipStream_t a, b;
+    ~Drain() {
+      (void)hipStreamSynchronize(a);
+      (void)hipStreamSynchronize(b);
+    }
+  } drain{us, cs};
   const int nbuf = (int)std::min<int64_t>(NB, (nb + ch - 1) / std::max<int64_t>(ch, 1));
   for (int k = 0; k < nbuf; ++k) {  // every buffer lives on the compute stream (allocated, used, freed there)
     HIP_TRY(th[k].alloc((size_t)ch * ld, cs));
@@ -504,10 +550,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
     od.trace_len = want_tr ? o->trace_len : 0;
     mcpx_desc dd = *d;
     dd.batch = cn;
-    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, cs, mod, wg))) {
-      (void)hipStreamSynchronize(us);  // no upload may still target a buffer freed on return
-      return rc;
-    }
+    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, cs, mod, wg))) return rc;
     HIP_TRY(hipEventRecord(P->consumed[k], cs));
   }
   HIP_TRY(hipStreamSynchronize(us));
@@ -531,18 +574,54 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
 
 // ---- sensitivities (src/AutoDiff.jl) ----------------------------------------
 
-// Validates a sensitivity call; fills the scalar part of the args and the kernel width.
-int prepare_sens(const mcpx_desc* d, mcpx::SensArgs* a, int* nmax) {
+// How a sensitivity call runs: one wave per instance (QP / affine, n + 2m ≤ 64: the
+// register kernels of sens_kernel_impl.hpp, `nmax` wide) or one workgroup per instance
+// (larger QP / affine systems in the dimension bucket `nv`, and every generated module).
+struct SensPlan {
+  int nmax = 0;
+  bool wg = false;
+  int nv = 0;
+  mcpx_module* mod = nullptr;
+};
+
+// Validates a sensitivity call; fills the scalar part of the args and the plan.
+int prepare_sens(const mcpx_desc* d, mcpx::SensArgs* a, SensPlan* plan, bool jvp, mcpx_module* mod = nullptr) {
   if (!d) return fail(MCPX_EINVAL, "desc must be non-NULL");
-  const int64_t pd = mcpx_theta_dim(d->family, d->n, d->m);
+  int64_t pd;
+  if (mod) {
+    if (d->family != MCPX_FAMILY_NONLINEAR)
+      return fail(MCPX_EINVAL, "a generated module differentiates family MCPX_FAMILY_NONLINEAR (got %d)", d->family);
+    if (d->n != mod->meta[1] || d->m != mod->meta[2])
+      return fail(MCPX_EINVAL, "desc (n=%d, m=%d) does not match the module (n=%d, m=%d)", d->n, d->m,
+                  mod->meta[1], mod->meta[2]);
+    pd = mod->meta[3];
+  } else {
+    if (d->family == MCPX_FAMILY_NONLINEAR)
+      return fail(MCPX_EINVAL, "family MCPX_FAMILY_NONLINEAR is differentiated through its generated module "
+                  "(mcpx_vjp_batch_module / mcpx_jvp_batch_module)");
+    pd = mcpx_theta_dim(d->family, d->n, d->m);
+  }
   if (pd < 0) return fail(MCPX_EINVAL, "bad family %d or negative dimensions (n=%d, m=%d)", d->family, d->n, d->m);
   if (d->n + d->m < 1) return fail(MCPX_EINVAL, "empty problem (n = m = 0)");
   if (d->batch < 0) return fail(MCPX_EINVAL, "negative batch");
   if (d->theta_ld < pd) return fail(MCPX_EINVAL, "theta_ld %lld < parameter dimension %lld", (long long)d->theta_ld, (long long)pd);
   const int N = d->n + 2 * d->m;
-  *nmax = pick_nmax(N);
-  if (*nmax < 0 || N > MCPX_MAX_KKT_DIM)
-    return fail(MCPX_EUNSUPPORTED, "sensitivities need n + 2m <= %d (got n=%d m=%d)", MCPX_MAX_KKT_DIM, d->n, d->m);
+  *plan = SensPlan{};
+  plan->mod = mod;
+  if (mod) {
+    const int bit = jvp ? MCPX_MODULE_JVP : MCPX_MODULE_VJP;
+    if (!((mod->meta[5] >> bit) & 1))
+      return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel (n=%d m=%d: its LDS footprint does not fit)",
+                  jvp ? "JVP" : "VJP", d->n, d->m);
+    plan->wg = true;
+  } else if (N <= MCPX_MAX_KKT_DIM) {
+    plan->nmax = pick_nmax(N);
+  } else if (N <= MCPX_MAX_WG_KKT_DIM) {
+    plan->wg = true;
+    plan->nv = pick_wg_bucket(N);
+  } else {
+    return fail(MCPX_EUNSUPPORTED, "sensitivities need n + 2m <= %d (got n=%d m=%d)", MCPX_MAX_WG_KKT_DIM, d->n, d->m);
+  }
   std::memset(a, 0, sizeof *a);
   a->theta_ld = d->theta_ld;
   a->p = pd;
@@ -552,10 +631,100 @@ int prepare_sens(const mcpx_desc* d, mcpx::SensArgs* a, int* nmax) {
   return MCPX_OK;
 }
 
-// Enqueue VJP (jvp = false) or JVP launches over the batch in chunks of 2^30 instances.
-int launch_sens(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, int nmax, const double* theta, const double* x,
-                const double* y, const double* s, const double* gx, const double* gy, const double* gs,
-                const double* tdot, double* out, int32_t* status, hipStream_t st) {
+// Workgroup-per-instance sensitivity launch (sens_wg_impl.hpp): persistent grid of the
+// resident workgroups on an atomic work queue, per-slot HBM workspace for [K | rhs]
+// (and a module's Jacobian blocks and ∇F_θ), allocated stream-ordered for this call.
+int launch_sens_wg_impl(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, const SensPlan& plan, hipStream_t st) {
+  const int n = d->n, m = d->m, N = n + 2 * m, nr = n + m;
+  const int ns = jvp ? N : nr;
+  const int K = a.n_partials;
+  const int nrhs = jvp ? std::max(1, std::min(K, MCPX_JVP_RHS)) : 1;
+  hipFunction_t f = nullptr;
+  const void* kp = nullptr;
+  int per_cu = 0;
+  if (plan.mod) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    hipModule_t hm;
+    const int rc = module_on(plan.mod, dev, &hm);
+    if (rc) return rc;
+    const char* name = jvp ? "mcpx_nl_jvp_wg" : "mcpx_nl_vjp_wg";
+    if (hipModuleGetFunction(&f, hm, name) != hipSuccess)
+      return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel", name);
+    HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, mcpx::wg::kThreads, 0));
+  } else {
+    kp = mcpx::sens_wg_kernel(a.family, jvp, plan.nv);
+    if (!kp) return fail(MCPX_EUNSUPPORTED, "no workgroup sensitivity kernel for family %d, dim %d", a.family, plan.nv);
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, mcpx::wg::kThreads, 0));
+  }
+  int dev = 0, cus = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t slots_max = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+  auto align = [](int64_t v) { return (v + 31) / 32 * 32; };  // 256-B boundaries
+  mcpx::wg::WgSensArgs w{};
+  w.ld = ns + nrhs;
+  w.nrhs = nrhs;
+  w.off_blk = align((int64_t)ns * w.ld);
+  w.off_dth = align(w.off_blk + (plan.mod ? plan.mod->meta[6] : 0));
+  w.off_sol = align(w.off_dth + (plan.mod ? (int64_t)nr * a.p : 0));
+  w.slot_stride = align(w.off_sol + (jvp ? (int64_t)nrhs * ns : 0));
+  const int64_t CH = (int64_t)1 << 30;
+  const int64_t grid_max = std::min(slots_max, std::min(CH, d->batch));
+  double* ws = nullptr;
+  const size_t bytes = sizeof(double) * (size_t)(grid_max * w.slot_stride) + 256;
+  HIP_TRY(pool_malloc((void**)&ws, bytes, st));
+  w.work = ws;
+  w.counter = (int32_t*)(ws + grid_max * w.slot_stride);
+  int rc = MCPX_OK;
+  for (int64_t b0 = 0; b0 < d->batch && rc == MCPX_OK; b0 += CH) {
+    const int64_t nb = std::min(CH, d->batch - b0);
+    const int grid = (int)std::min(grid_max, nb);
+    w.s = a;
+    w.s.theta = a.theta + b0 * d->theta_ld;
+    w.s.x = a.x + b0 * n;
+    w.s.y = a.y + b0 * m;
+    w.s.s = a.s + b0 * m;
+    w.s.gx = a.gx ? a.gx + b0 * n : nullptr;
+    w.s.gy = a.gy ? a.gy + b0 * m : nullptr;
+    w.s.gs = a.gs ? a.gs + b0 * m : nullptr;
+    w.s.theta_dot = a.theta_dot ? a.theta_dot + b0 * K * a.p : nullptr;
+    w.s.out = a.out + (jvp ? b0 * K * N : b0 * a.p);
+    w.s.status = a.status ? a.status + b0 : nullptr;
+    w.batch = nb;
+    hipError_t e = hipMemsetAsync(w.counter, 0, sizeof(int32_t), st);
+    if (e == hipSuccess) {
+      if (plan.mod) {
+        void* params[] = {&w};
+        e = hipModuleLaunchKernel(f, (unsigned)grid, 1, 1, mcpx::wg::kThreads, 1, 1, 0, st, params, nullptr);
+      } else {
+        e = mcpx::launch_sens_wg(a.family, jvp, plan.nv, w, grid, st);
+      }
+    }
+    if (e != hipSuccess) rc = fail(MCPX_EHIP, "workgroup sensitivity launch failed: %s", hipGetErrorString(e));
+  }
+  HIP_TRY(hipFreeAsync(ws, st));
+  return rc;
+}
+
+// Enqueue VJP (jvp = false) or JVP launches over the batch: the one-wave kernels in
+// chunks of 2^30 instances, or the workgroup kernels.
+int launch_sens(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, const SensPlan& plan, const double* theta,
+                const double* x, const double* y, const double* s, const double* gx, const double* gy,
+                const double* gs, const double* tdot, double* out, int32_t* status, hipStream_t st) {
+  if (plan.wg) {
+    a.theta = theta;
+    a.x = x;
+    a.y = y;
+    a.s = s;
+    a.gx = gx;
+    a.gy = gy;
+    a.gs = gs;
+    a.theta_dot = tdot;
+    a.out = out;
+    a.status = status;
+    return launch_sens_wg_impl(jvp, d, a, plan, st);
+  }
   const int64_t CH = (int64_t)1 << 30;
   const int n = d->n, m = d->m, N = n + 2 * m, K = a.n_partials;
   for (int64_t b0 = 0; b0 < d->batch; b0 += CH) {
@@ -571,15 +740,16 @@ int launch_sens(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, int nmax, const 
     a.out = out + (jvp ? b0 * K * N : b0 * a.p);
     a.status = status ? status + b0 : nullptr;
     // the VJP factors the slack-eliminated (n+m)-dim system, the JVP the full n+2m
-    HIP_TRY(jvp ? mcpx::launch_jvp(nmax, a, nb, st) : mcpx::launch_vjp(pick_nmax(n + m), a, nb, st));
+    HIP_TRY(jvp ? mcpx::launch_jvp(plan.nmax, a, nb, st) : mcpx::launch_vjp(pick_nmax(n + m), a, nb, st));
   }
   return MCPX_OK;
 }
 
 // One device's share [b0, b0+nb) of a host-buffer sensitivity call.
-int sens_shard(bool jvp, int dev, const mcpx_desc* d, const mcpx::SensArgs& a0, int nmax, const double* theta,
-               const double* x, const double* y, const double* s, const double* gx, const double* gy,
-               const double* gs, const double* tdot, double* out, int32_t* status, int64_t b0, int64_t nb) {
+int sens_shard(bool jvp, int dev, const mcpx_desc* d, const mcpx::SensArgs& a0, const SensPlan& plan,
+               const double* theta, const double* x, const double* y, const double* s, const double* gx,
+               const double* gy, const double* gs, const double* tdot, double* out, int32_t* status, int64_t b0,
+               int64_t nb) {
   HIP_TRY(hipSetDevice(dev));
   int rc = check_device(dev);
   if (rc) return rc;
@@ -605,17 +775,22 @@ int sens_shard(bool jvp, int dev, const mcpx_desc* d, const mcpx::SensArgs& a0, 
   const double* bx = dx.p ? dx.p : th.p;
   const double* by = dy.p ? dy.p : th.p;
   const double* bs = ds.p ? ds.p : th.p;
-  if ((rc = launch_sens(jvp, &dd, a0, nmax, th.p, bx, by, bs, gx ? dgx.p : nullptr, gy ? dgy.p : nullptr,
-                        gs ? dgs.p : nullptr, dtd.p, dout.p, status ? dst.p : nullptr, nullptr)))
+  // an empty output (p = 0, or K = 0) still needs a valid base pointer
+  double* bo = dout.p ? dout.p : (double*)th.p;
+  if ((rc = launch_sens(jvp, &dd, a0, plan, th.p, bx, by, bs, gx ? dgx.p : nullptr, gy ? dgy.p : nullptr,
+                        gs ? dgs.p : nullptr, dtd.p, bo, status ? dst.p : nullptr, nullptr))) {
+    (void)hipDeviceSynchronize();  // nothing may still run on the buffers freed on return
     return rc;
+  }
   HIP_TRY(hipDeviceSynchronize());
   if (per_out) HIP_TRY(hipMemcpy(out + b0 * per_out, dout.p, sizeof(double) * nb * per_out, hipMemcpyDeviceToHost));
   if (status) HIP_TRY(hipMemcpy(status + b0, dst.p, sizeof(int32_t) * nb, hipMemcpyDeviceToHost));
   return MCPX_OK;
 }
 
-// Host-buffer entry shared by mcpx_vjp_batch / mcpx_jvp_batch: contiguous shards, one thread per device.
-int sens_host(bool jvp, const mcpx_desc* d, const mcpx::SensArgs& a, int nmax, const double* theta,
+// Host-buffer entry shared by mcpx_vjp_batch / mcpx_jvp_batch (and the module variants):
+// contiguous shards, one thread per device.
+int sens_host(bool jvp, const mcpx_desc* d, const mcpx::SensArgs& a, const SensPlan& plan, const double* theta,
               const double* x, const double* y, const double* s, const double* gx, const double* gy,
               const double* gs, const double* tdot, int num_devices, double* out, int32_t* status) {
   const int avail = mcpx_device_count();
@@ -630,7 +805,7 @@ int sens_host(bool jvp, const mcpx_desc* d, const mcpx::SensArgs& a, int nmax, c
   std::vector<std::thread> th;
   for (int g = 0; g < num_devices; ++g)
     th.emplace_back([&, g] {
-      rcs[g] = sens_shard(jvp, g, d, a, nmax, theta, x, y, s, gx, gy, gs, tdot, out, status, start[g],
+      rcs[g] = sens_shard(jvp, g, d, a, plan, theta, x, y, s, gx, gy, gs, tdot, out, status, start[g],
                           start[g + 1] - start[g]);
       if (rcs[g]) errs[g] = g_err;
     });
@@ -645,6 +820,69 @@ int sens_inputs_ok(const mcpx_desc* d, const double* theta, const double* x, con
   if (!theta || !out) return fail(MCPX_EINVAL, "theta and the output array must be non-NULL");
   if ((d->n > 0 && !x) || (d->m > 0 && (!y || !s))) return fail(MCPX_EINVAL, "solution arrays x/y/s must be non-NULL");
   return MCPX_OK;
+}
+
+int vjp_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                    const double* s, const double* gx, const double* gy, const double* gs, double* dtheta,
+                    int32_t* status, void* stream) {
+  mcpx::SensArgs a;
+  SensPlan plan;
+  int rc;
+  if ((rc = prepare_sens(d, &a, &plan, false, mod))) return rc;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, dtheta))) return rc;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if ((rc = check_device(dev))) return rc;
+  return launch_sens(false, d, a, plan, theta, x ? x : theta, y ? y : theta, s ? s : theta, gx, gy, gs, nullptr,
+                     dtheta, status, (hipStream_t)stream);
+}
+
+int vjp_host_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                  const double* s, const double* gx, const double* gy, const double* gs, int num_devices,
+                  double* dtheta, int32_t* status) {
+  mcpx::SensArgs a;
+  SensPlan plan;
+  int rc;
+  if ((rc = prepare_sens(d, &a, &plan, false, mod))) return rc;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, dtheta))) return rc;
+  return sens_host(false, d, a, plan, theta, x, y, s, gx, gy, gs, nullptr, num_devices, dtheta, status);
+}
+
+int jvp_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                    const double* s, int32_t n_partials, const double* theta_dot, double* zdot, int32_t* status,
+                    void* stream) {
+  mcpx::SensArgs a;
+  SensPlan plan;
+  int rc;
+  if ((rc = prepare_sens(d, &a, &plan, true, mod))) return rc;
+  if (n_partials < 0) return fail(MCPX_EINVAL, "negative n_partials");
+  a.n_partials = n_partials;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, zdot))) return rc;
+  if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if ((rc = check_device(dev))) return rc;
+  return launch_sens(true, d, a, plan, theta, x ? x : theta, y ? y : theta, s ? s : theta, nullptr, nullptr,
+                     nullptr, theta_dot, zdot, status, (hipStream_t)stream);
+}
+
+int jvp_host_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                  const double* s, int32_t n_partials, const double* theta_dot, int num_devices, double* zdot,
+                  int32_t* status) {
+  mcpx::SensArgs a;
+  SensPlan plan;
+  int rc;
+  if ((rc = prepare_sens(d, &a, &plan, true, mod))) return rc;
+  if (n_partials < 0) return fail(MCPX_EINVAL, "negative n_partials");
+  a.n_partials = n_partials;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, zdot))) return rc;
+  if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
+  return sens_host(true, d, a, plan, theta, x, y, s, nullptr, nullptr, nullptr, theta_dot, num_devices, zdot,
+                   status);
 }
 
 // mcpx_solve_batch_device / mcpx_solve_batch_module_device (mod = nullptr: QP / affine kernels).
@@ -760,59 +998,52 @@ int mcpx_host_unregister(void* ptr) {
 int mcpx_vjp_batch_device(const mcpx_desc* d, const double* theta, const double* x, const double* y,
                           const double* s, const double* gx, const double* gy, const double* gs, double* dtheta,
                           int32_t* status, void* stream) {
-  mcpx::SensArgs a;
-  int nmax, rc;
-  if ((rc = prepare_sens(d, &a, &nmax))) return rc;
-  if (d->batch == 0) return MCPX_OK;
-  if ((rc = sens_inputs_ok(d, theta, x, y, s, dtheta))) return rc;
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if ((rc = check_device(dev))) return rc;
-  return launch_sens(false, d, a, nmax, theta, x ? x : theta, y ? y : theta, s ? s : theta, gx, gy, gs, nullptr,
-                     dtheta, status, (hipStream_t)stream);
+  return vjp_device_impl(nullptr, d, theta, x, y, s, gx, gy, gs, dtheta, status, stream);
 }
 
 int mcpx_vjp_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y, const double* s,
                    const double* gx, const double* gy, const double* gs, int num_devices, double* dtheta,
                    int32_t* status) {
-  mcpx::SensArgs a;
-  int nmax, rc;
-  if ((rc = prepare_sens(d, &a, &nmax))) return rc;
-  if (d->batch == 0) return MCPX_OK;
-  if ((rc = sens_inputs_ok(d, theta, x, y, s, dtheta))) return rc;
-  return sens_host(false, d, a, nmax, theta, x, y, s, gx, gy, gs, nullptr, num_devices, dtheta, status);
+  return vjp_host_impl(nullptr, d, theta, x, y, s, gx, gy, gs, num_devices, dtheta, status);
 }
 
 int mcpx_jvp_batch_device(const mcpx_desc* d, const double* theta, const double* x, const double* y,
                           const double* s, int32_t n_partials, const double* theta_dot, double* zdot,
                           int32_t* status, void* stream) {
-  mcpx::SensArgs a;
-  int nmax, rc;
-  if ((rc = prepare_sens(d, &a, &nmax))) return rc;
-  if (n_partials < 0) return fail(MCPX_EINVAL, "negative n_partials");
-  a.n_partials = n_partials;
-  if (d->batch == 0) return MCPX_OK;
-  if ((rc = sens_inputs_ok(d, theta, x, y, s, zdot))) return rc;
-  if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if ((rc = check_device(dev))) return rc;
-  return launch_sens(true, d, a, nmax, theta, x ? x : theta, y ? y : theta, s ? s : theta, nullptr, nullptr,
-                     nullptr, theta_dot, zdot, status, (hipStream_t)stream);
+  return jvp_device_impl(nullptr, d, theta, x, y, s, n_partials, theta_dot, zdot, status, stream);
 }
 
 int mcpx_jvp_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y, const double* s,
                    int32_t n_partials, const double* theta_dot, int num_devices, double* zdot, int32_t* status) {
-  mcpx::SensArgs a;
-  int nmax, rc;
-  if ((rc = prepare_sens(d, &a, &nmax))) return rc;
-  if (n_partials < 0) return fail(MCPX_EINVAL, "negative n_partials");
-  a.n_partials = n_partials;
-  if (d->batch == 0) return MCPX_OK;
-  if ((rc = sens_inputs_ok(d, theta, x, y, s, zdot))) return rc;
-  if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
-  return sens_host(true, d, a, nmax, theta, x, y, s, nullptr, nullptr, nullptr, theta_dot, num_devices, zdot,
-                   status);
+  return jvp_host_impl(nullptr, d, theta, x, y, s, n_partials, theta_dot, num_devices, zdot, status);
+}
+
+int mcpx_vjp_batch_module(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x,
+                          const double* y, const double* s, const double* gx, const double* gy, const double* gs,
+                          int num_devices, double* dtheta, int32_t* status) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  return vjp_host_impl(mod, d, theta, x, y, s, gx, gy, gs, num_devices, dtheta, status);
+}
+
+int mcpx_vjp_batch_module_device(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x,
+                                 const double* y, const double* s, const double* gx, const double* gy,
+                                 const double* gs, double* dtheta, int32_t* status, void* stream) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  return vjp_device_impl(mod, d, theta, x, y, s, gx, gy, gs, dtheta, status, stream);
+}
+
+int mcpx_jvp_batch_module(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x,
+                          const double* y, const double* s, int32_t n_partials, const double* theta_dot,
+                          int num_devices, double* zdot, int32_t* status) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  return jvp_host_impl(mod, d, theta, x, y, s, n_partials, theta_dot, num_devices, zdot, status);
+}
+
+int mcpx_jvp_batch_module_device(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x,
+                                 const double* y, const double* s, int32_t n_partials, const double* theta_dot,
+                                 double* zdot, int32_t* status, void* stream) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  return jvp_device_impl(mod, d, theta, x, y, s, n_partials, theta_dot, zdot, status, stream);
 }
 
 // ---- generated nonlinear modules (MCPX_FAMILY_NONLINEAR) ----------------------

@@ -83,7 +83,8 @@ class OracleNL(C.Structure):
 
     _fields_ = [("init", C.c_void_p), ("eval", C.c_void_p), ("p", C.c_int32), ("has_s", C.c_int32),
                 ("size", C.c_int32), ("pad_", C.c_int32), ("qk_ptr", C.c_void_p), ("qk_idx", C.c_void_p),
-                ("rj_ptr", C.c_void_p), ("rj_idx", C.c_void_p)]
+                ("rj_ptr", C.c_void_p), ("rj_idx", C.c_void_p), ("eval_theta", C.c_void_p),
+                ("tc_ptr", C.c_void_p), ("tc_idx", C.c_void_p), ("tr_ptr", C.c_void_p), ("tr_idx", C.c_void_p)]
 
 
 _GEN_DIR = os.path.join(_HERE, "_build", "gen")
@@ -107,9 +108,13 @@ def nl_lib(nl):
             f.write("\nvoid oracle_nl_init(const double* th, double* blk) { mcpx_nl_init(th, blk); }\n"
                     "void oracle_nl_eval(const double* th, const double* z, double* blk) "
                     "{ mcpx_nl_eval(th, z, blk); }\n"
+                    "void oracle_nl_eval_theta(const double* th, const double* z, double* dth) "
+                    "{ mcpx_nl_eval_theta(th, z, dth); }\n"
                     "const int32_t* oracle_nl_table(int which) {\n"
                     "  switch (which) { case 0: return mcpx_nl_qk_ptr; case 1: return mcpx_nl_qk_idx;\n"
-                    "    case 2: return mcpx_nl_rj_ptr; default: return mcpx_nl_rj_idx; }\n}\n")
+                    "    case 2: return mcpx_nl_rj_ptr; case 3: return mcpx_nl_rj_idx;\n"
+                    "    case 4: return mcpx_nl_tc_ptr; case 5: return mcpx_nl_tc_idx;\n"
+                    "    case 6: return mcpx_nl_tr_ptr; default: return mcpx_nl_tr_idx; }\n}\n")
         tmp = f"{so}.{os.getpid()}.tmp"
         subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
                         "-o", tmp, src, "-lm"], check=True)
@@ -117,6 +122,16 @@ def nl_lib(nl):
     L = C.CDLL(so)
     _nl_libs[nl.key] = L
     return L
+
+
+def _nl_spec(nl) -> OracleNL:
+    G = nl_lib(nl)
+    G.oracle_nl_table.restype = C.c_void_p
+    G.oracle_nl_table.argtypes = [C.c_int]
+    fn = lambda f: C.cast(f, C.c_void_p).value
+    t = [G.oracle_nl_table(w) for w in range(8)]
+    return OracleNL(fn(G.oracle_nl_init), fn(G.oracle_nl_eval), nl.p, int(nl.has_s), nl.size, 0, *t[:4],
+                    fn(G.oracle_nl_eval_theta), *t[4:])
 
 
 def solve_batch_nl(nl, theta: np.ndarray, *, x0=None, y0=None, s0=None, params: Params | None = None,
@@ -143,11 +158,7 @@ def solve_batch_nl(nl, theta: np.ndarray, *, x0=None, y0=None, s0=None, params: 
               _ptr(r["outer_iters"]), _ptr(r["status"]), _ptr(r["newton_iters"]),
               _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
               int(trace_len), 0)
-    G = nl_lib(nl)
-    G.oracle_nl_table.restype = C.c_void_p
-    G.oracle_nl_table.argtypes = [C.c_int]
-    spec = OracleNL(C.cast(G.oracle_nl_init, C.c_void_p).value, C.cast(G.oracle_nl_eval, C.c_void_p).value,
-                    nl.p, int(nl.has_s), nl.size, 0, *(G.oracle_nl_table(w) for w in range(4)))
+    spec = _nl_spec(nl)
     L = lib()
     L.oracle_solve_batch_nl.restype = C.c_int
     L.oracle_solve_batch_nl.argtypes = [C.POINTER(Desc), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -208,4 +219,57 @@ def jvp_batch(family: int, n: int, m: int, theta, x, y, s, theta_dot, nthreads: 
                                       _ptr(zd), _ptr(st), int(nthreads))
     if rc != 0:
         raise ValueError(f"oracle_jvp_batch failed with code {rc}")
+    return zd, st
+
+
+def _sens_nl_lib():
+    L = lib()
+    if not hasattr(L, "_sens_nl_ready"):
+        L.oracle_vjp_batch_nl.restype = C.c_int
+        L.oracle_vjp_batch_nl.argtypes = [C.POINTER(Desc)] + [C.c_void_p] * 9 + [C.c_int, C.POINTER(OracleNL)]
+        L.oracle_jvp_batch_nl.restype = C.c_int
+        L.oracle_jvp_batch_nl.argtypes = [C.POINTER(Desc), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                          C.POINTER(OracleNL)]
+        L._sens_nl_ready = True
+    return L
+
+
+def vjp_batch_nl(nl, theta, x, y, s, gx=None, gy=None, gs=None, nthreads: int = 1):
+    """Oracle of mcpx_vjp_batch_module: returns (dtheta (B, p), status (B,))."""
+    from mcp_amd._abi import FAMILY_NONLINEAR
+
+    theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+    B, ld = theta.shape
+    n, m, p = nl.n, nl.m, nl.p
+    x, y, s = _f64(x, (B, n)), _f64(y, (B, m)), _f64(s, (B, m))
+    gx, gy, gs = _f64(gx, (B, n)), _f64(gy, (B, m)), _f64(gs, (B, m))
+    dth = np.empty((B, p))
+    st = np.empty(B, np.int32)
+    desc = Desc(FAMILY_NONLINEAR, n, m, 0, B, ld)
+    rc = _sens_nl_lib().oracle_vjp_batch_nl(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), _ptr(gx),
+                                            _ptr(gy), _ptr(gs), _ptr(dth), _ptr(st), int(nthreads),
+                                            C.byref(_nl_spec(nl)))
+    if rc != 0:
+        raise ValueError(f"oracle_vjp_batch_nl failed with code {rc}")
+    return dth, st
+
+
+def jvp_batch_nl(nl, theta, x, y, s, theta_dot, nthreads: int = 1):
+    """Oracle of mcpx_jvp_batch_module: theta_dot (B, K, p) → (zdot (B, K, n+2m), status (B,))."""
+    from mcp_amd._abi import FAMILY_NONLINEAR
+
+    theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+    B, ld = theta.shape
+    n, m, p = nl.n, nl.m, nl.p
+    td = np.ascontiguousarray(theta_dot, dtype=np.float64).reshape(B, -1, p)
+    K = td.shape[1]
+    x, y, s = _f64(x, (B, n)), _f64(y, (B, m)), _f64(s, (B, m))
+    zd = np.empty((B, K, n + 2 * m))
+    st = np.empty(B, np.int32)
+    desc = Desc(FAMILY_NONLINEAR, n, m, 0, B, ld)
+    rc = _sens_nl_lib().oracle_jvp_batch_nl(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), int(K),
+                                            _ptr(td), _ptr(zd), _ptr(st), int(nthreads), C.byref(_nl_spec(nl)))
+    if rc != 0:
+        raise ValueError(f"oracle_jvp_batch_nl failed with code {rc}")
     return zd, st

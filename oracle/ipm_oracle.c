@@ -92,6 +92,12 @@ typedef struct oracle_nl {
   /* structural nonzeros (mcp_amd/codegen.py NLSystem.structure): K(i) of row i of
    * Q = ∂G/∂y and J(k) of row k of R = ∂H/∂x, CSR with ascending indices */
   const int32_t *qk_ptr, *qk_idx, *rj_ptr, *rj_idx;
+  /* ∇F_θ of the G/H rows (src/mcp.jl:122-147): eval_theta writes the structural nonzeros
+   * of the (n+m)×p column-major block dth[t·(n+m) + i] at z = [x; y]; tc = rows of
+   * column t, tr = columns of row i (CSR, ascending).  Sensitivities only (may be NULL
+   * for a solve). */
+  void (*eval_theta)(const double* th, const double* z, double* dth);
+  const int32_t *tc_ptr, *tc_idx, *tr_ptr, *tr_idx;
 } oracle_nl;
 
 /* doubles of the block array, the S block always included (zero when absent) */
@@ -674,6 +680,7 @@ static double dtheta_row(int family, int n, int m, const double* d, const double
 
 typedef struct sens_ws {
   double *J, *JT, *b, *dz, *z, *row;
+  double *blk, *dth; /* MCPX_FAMILY_NONLINEAR: generated blocks and ∇F_θ */
   int *rem, *step, *prow;
 } sens_ws;
 
@@ -688,12 +695,28 @@ static int sens_ws_alloc(sens_ws* w, int N) {
   w->rem = (int*)malloc(sizeof(int) * NN);
   w->step = (int*)malloc(sizeof(int) * NN);
   w->prow = (int*)malloc(sizeof(int) * NN);
+  w->blk = NULL;
+  w->dth = NULL;
   return !(w->J && w->JT && w->b && w->dz && w->z && w->row && w->rem && w->step && w->prow);
 }
 
 static void sens_ws_free(sens_ws* w) {
   free(w->J); free(w->JT); free(w->b); free(w->dz); free(w->z); free(w->row);
   free(w->rem); free(w->step); free(w->prow);
+  free(w->blk); free(w->dth);
+}
+
+/* MCPX_FAMILY_NONLINEAR: (∇F_θ θ̇)_i from the generated block, θ columns of row i
+ * ascending (tr); 0 for the s⊙y − ϵ rows. */
+static double dtheta_row_nl(const oracle_nl* nl, int n, int m, const double* dth, const double* d, int i) {
+  if (i >= n + m) return 0.0;
+  const int nr = n + m;
+  double acc = 0.0;
+  for (int u = nl->tr_ptr[i]; u < nl->tr_ptr[i + 1]; ++u) {
+    const int t = nl->tr_idx[u];
+    acc = fma(dth[(size_t)t * nr + i], d[t], acc);
+  }
+  return acc;
 }
 
 /* ∇F_z (no tol·I) at z, N×N row-major, via family_row (src/mcp.jl:97-120). */
@@ -709,6 +732,8 @@ typedef struct sens_job {
   int K;
   double* out;
   int32_t* status;
+  const oracle_nl* nl; /* MCPX_FAMILY_NONLINEAR, else NULL */
+  int64_t p;           /* θ dimension (dense stride of dtheta / theta_dot) */
   int64_t next;
   pthread_mutex_t mu;
   int err;
@@ -718,11 +743,22 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
   const mcpx_desc* d = j->d;
   const int n = d->n, m = d->m, N = n + 2 * m;
   const double* th = j->theta + b * d->theta_ld;
-  const int64_t p = oracle_theta_dim(d->family, n, m);
+  const int64_t p = j->p;
   for (int i = 0; i < n; ++i) w->z[i] = j->x[b * n + i];
   for (int k = 0; k < m; ++k) {
     w->z[n + k] = j->y[b * m + k];
     w->z[n + m + k] = j->s[b * m + k];
+  }
+  /* MCPX_FAMILY_NONLINEAR: ∇F_z from the generated blocks at z (family_row reads them as
+     the affine family reads θ), ∇F_θ from the generated eval_theta */
+  const double* fth = th;
+  if (j->nl) {
+    memset(w->blk, 0, sizeof(double) * nl_blk_doubles(n, m));
+    j->nl->init(th, w->blk);
+    j->nl->eval(th, w->z, w->blk);
+    memset(w->dth, 0, sizeof(double) * (size_t)(n + m) * (size_t)(p > 0 ? p : 1));
+    j->nl->eval_theta(th, w->z, w->dth);
+    fth = w->blk;
   }
   const double nanv = __builtin_nan("");
   int failed = 0;
@@ -736,20 +772,25 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
                      + Σ_k ∇F_z[n+k][n+q] gs_k
        (gs = NULL: the Σ gs chains are skipped), factored by lu_solve like the solver's
        REDUCED Newton system.  The GPU's vjp_kernel forms the same rows. */
-    jacobian_z(d->family, n, m, th, w->z, w->J);
+    jacobian_z(d->family, n, m, fth, w->z, w->J);
     const int Nr = n + m;
     const double* yv = w->z + n;
     const double* sv = w->z + n + m;
     for (int r = 0; r < Nr; ++r) {
       double* row = w->JT + (size_t)r * Nr;
+      /* QP family, y-rows: ∂H/∂y ≡ 0 is a structural zero block — never multiplied, neither
+         into the row (0 instead of 0·y_k) nor into the rhs (no fma(0, gs_k, ·)); the kernel
+         (sens_kernel_impl.hpp vjp_reduced_row) skips the same terms, so Inf/NaN in y or gs
+         give the same bits on both sides */
+      const int qp_y = d->family == MCPX_FAMILY_QP && r >= n;
       for (int i = 0; i < n; ++i) row[i] = w->J[(size_t)i * N + r];
       for (int k = 0; k < m; ++k) {
-        double v = w->J[(size_t)(n + k) * N + r] * yv[k];
+        double v = qp_y ? 0.0 : w->J[(size_t)(n + k) * N + r] * yv[k];
         if (r == n + k) v = v + sv[k];
         row[n + k] = v;
       }
       double acc = r < n ? (j->gx ? j->gx[b * n + r] : 0.0) : (j->gy ? j->gy[b * m + (r - n)] : 0.0);
-      if (j->gs)
+      if (j->gs && !qp_y)
         for (int k = 0; k < m; ++k) acc = fma(w->J[(size_t)(n + k) * N + r], j->gs[b * m + k], acc);
       w->b[r] = acc;
     }
@@ -768,7 +809,19 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
     const double* y = w->z + n;
     double* o = j->out + b * p;
     const size_t nn = (size_t)n * n, nm = (size_t)n * m, mm = (size_t)m * m;
-    if (d->family == MCPX_FAMILY_QP) {
+    if (j->nl) {
+      /* ∂θ_t = −Σ_i ∇F_θ[i, t] λ_i over the structural nonzeros of column t, rows ascending
+         (λ = [λx; λh]: the G rows, then the H − s rows) */
+      const int nr = n + m;
+      for (int64_t t = 0; t < p; ++t) {
+        double acc = 0.0;
+        for (int u = j->nl->tc_ptr[t]; u < j->nl->tc_ptr[t + 1]; ++u) {
+          const int i = j->nl->tc_idx[u];
+          acc = fma(w->dth[(size_t)t * nr + i], w->dz[i], acc);
+        }
+        o[t] = failed ? nanv : -acc;
+      }
+    } else if (d->family == MCPX_FAMILY_QP) {
       for (int c = 0; c < n; ++c)
         for (int r = 0; r < n; ++r) o[(size_t)c * n + r] = -(lx[r] * x[c]);               /* ∂M_rc */
       for (int c = 0; c < n; ++c)
@@ -792,8 +845,9 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
     for (int c = 0; c < j->K; ++c) {
       const double* dd = j->tdot + (b * j->K + c) * p;
       double* o = j->out + (b * j->K + c) * N;
-      jacobian_z(d->family, n, m, th, w->z, w->J);
-      for (int i = 0; i < N; ++i) w->b[i] = -dtheta_row(d->family, n, m, dd, w->z, i);
+      jacobian_z(d->family, n, m, fth, w->z, w->J);
+      for (int i = 0; i < N; ++i)
+        w->b[i] = j->nl ? -dtheta_row_nl(j->nl, n, m, w->dth, dd, i) : -dtheta_row(d->family, n, m, dd, w->z, i);
       const int f = lu_solve(N, w->J, w->b, w->dz, w->rem, w->step, w->prow);
       failed |= f;
       for (int i = 0; i < N; ++i) o[i] = f ? nanv : w->dz[i];
@@ -805,7 +859,13 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
 static void* sens_worker(void* arg) {
   sens_job* j = (sens_job*)arg;
   sens_ws w;
-  if (sens_ws_alloc(&w, j->d->n + 2 * j->d->m)) {
+  int bad = sens_ws_alloc(&w, j->d->n + 2 * j->d->m);
+  if (!bad && j->nl) {
+    w.blk = (double*)malloc(sizeof(double) * (nl_blk_doubles(j->d->n, j->d->m) + 1));
+    w.dth = (double*)malloc(sizeof(double) * ((size_t)(j->d->n + j->d->m) * (size_t)(j->p > 0 ? j->p : 1) + 1));
+    bad = !w.blk || !w.dth;
+  }
+  if (bad) {
     pthread_mutex_lock(&j->mu);
     j->err = 1;
     pthread_mutex_unlock(&j->mu);
@@ -825,9 +885,12 @@ static void* sens_worker(void* arg) {
 
 static int sens_run(sens_job* j, int nthreads) {
   const mcpx_desc* d = j->d;
-  const int64_t pd = oracle_theta_dim(d->family, d->n, d->m);
+  const int64_t pd = j->nl ? j->nl->p : oracle_theta_dim(d->family, d->n, d->m);
   if (pd < 0 || d->n + d->m < 1 || d->batch < 0 || d->theta_ld < pd || !j->theta || !j->out) return MCPX_EINVAL;
-  if (d->n + 2 * d->m > MCPX_MAX_KKT_DIM) return MCPX_EUNSUPPORTED;
+  if (j->nl ? (d->family != MCPX_FAMILY_NONLINEAR || !j->nl->eval_theta || !j->nl->tc_ptr || !j->nl->tr_ptr)
+            : d->family == MCPX_FAMILY_NONLINEAR)
+    return MCPX_EINVAL;
+  j->p = pd;
   j->next = 0;
   j->err = 0;
   pthread_mutex_init(&j->mu, NULL);
@@ -853,6 +916,29 @@ int oracle_vjp_batch(const mcpx_desc* d, const double* theta, const double* x, c
   memset(&j, 0, sizeof j);
   j.jvp = 0; j.d = d; j.theta = theta; j.x = x; j.y = y; j.s = s;
   j.gx = gx; j.gy = gy; j.gs = gs; j.out = dtheta; j.status = status;
+  return sens_run(&j, nthreads);
+}
+
+/* MCPX_FAMILY_NONLINEAR: the same with the problem's generated ∇F_z / ∇F_θ code. */
+int oracle_vjp_batch_nl(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                        const double* s, const double* gx, const double* gy, const double* gs,
+                        double* dtheta, int32_t* status, int nthreads, const oracle_nl* nl) {
+  if (!d || !nl || !nl->init || !nl->eval) return MCPX_EINVAL;
+  sens_job j;
+  memset(&j, 0, sizeof j);
+  j.jvp = 0; j.d = d; j.theta = theta; j.x = x; j.y = y; j.s = s; j.nl = nl;
+  j.gx = gx; j.gy = gy; j.gs = gs; j.out = dtheta; j.status = status;
+  return sens_run(&j, nthreads);
+}
+
+int oracle_jvp_batch_nl(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                        const double* s, int32_t n_partials, const double* theta_dot, double* zdot,
+                        int32_t* status, int nthreads, const oracle_nl* nl) {
+  if (!d || !nl || !nl->init || !nl->eval || n_partials < 0 || (n_partials > 0 && !theta_dot)) return MCPX_EINVAL;
+  sens_job j;
+  memset(&j, 0, sizeof j);
+  j.jvp = 1; j.d = d; j.theta = theta; j.x = x; j.y = y; j.s = s; j.nl = nl;
+  j.tdot = theta_dot; j.K = n_partials; j.out = zdot; j.status = status;
   return sens_run(&j, nthreads);
 }
 

@@ -34,7 +34,33 @@ def test_solve_dims_and_executed_flops():
     assert bench.executed_flops(32, 16, "dense") == resid + bench.lu_flops(64)
     # m = 15: residual −2·(32 + 32), rr/δy −4·32, the Schur GEMM's K stays padded to 16
     assert bench.executed_flops(32, 16, "schur") - bench.executed_flops(32, 15, "schur") == 256
-    assert bench.roofline_bound("schur") == "valu"
+
+
+
+def test_roofline_bound_from_pmc():
+    """bound = the unit the PMC counters show busiest (≥ 0.3), else latency; without PMC
+    evidence of the build, the stated fallback, marked as assumed."""
+    assert bench.roofline_bound({}, 5.0, "valu")[0] == "valu"
+    assert "assumed" in bench.roofline_bound({}, 5.0, "valu")[1]["source"]
+    act = 1e7 * bench.XCDS  # 10 M cycles per XCD
+    sim = 1e7 * bench.SIMDS
+    valu = {"pmc": {"GRBM_GUI_ACTIVE": act, "SQ_INSTS_VALU": 0.8 * sim / 4, "SQ_VALU_MFMA_BUSY_CYCLES": 0.1 * sim,
+                    "FETCH_SIZE": 1e6, "WRITE_SIZE": 0.0, "_source": "x"}}
+    assert bench.roofline_bound(valu, 5.0, "hbm")[0] == "valu"
+    hbm = {"pmc": dict(valu["pmc"], SQ_INSTS_VALU=0.1 * sim / 4, FETCH_SIZE=5.0 * 8e12 / 1024 * 5e-3)}
+    b, e = bench.roofline_bound(hbm, 5.0, "valu")
+    assert b == "hbm" and e["utilisation"]["hbm"] == pytest.approx(5.0)
+    lat = {"pmc": dict(valu["pmc"], SQ_INSTS_VALU=0.05 * sim / 4)}
+    assert bench.roofline_bound(lat, 5.0, "valu")[0] == "latency"
+
+
+def test_parity_report_counts_instances():
+    got = {"x": np.array([[1.0, np.nan], [2.0, 3.0], [4.0, 5.0]]), "status": np.array([0, 1, 0], np.int32)}
+    ref = {"x": np.array([[1.0, np.nan], [2.0, 3.5], [4.0, 5.0]]), "status": np.array([0, 1, 1], np.int32)}
+    r = bench.parity_report(got, ref, ("x", "status"), 3, "t")
+    assert r["mismatches"] == {"x": 1, "status": 1} and not r["pass"] and r["bit_exact_fields"] == []
+    r = bench.parity_report(got, got, ("x", "status"), 3, "t")
+    assert r["pass"] and r["bit_exact_fields"] == ["x", "status"]
 
 
 def test_plan_strong_scaling_is_the_baseline_config():
@@ -91,7 +117,7 @@ def test_evidence_only_for_its_config_and_build(tmp_path, monkeypatch):
     ev = bench.evidence("x", cfg)
     assert set(ev) == {"pmc", "trace"}
     assert bench.pmc_traffic(ev)[0] == 1024.0 * 1024
-    r = bench.roofline(6.01, 78.6e9 * 6.01 * 0.5, 1e9, 1e9, ev, "k", "valu", "")
+    r = bench.roofline(6.01, 78.6e9 * 6.01 * 0.5, 1e9, 1e9, ev, "k", ("valu", {}), "")
     assert r["frac_trace"] == pytest.approx(0.5) and r["frac"] == pytest.approx(0.5)
     assert bench.evidence("x", dict(cfg, batch_per_gpu=8192)) == {}  # another configuration
     monkeypatch.setattr(b, "built_hash", lambda: "other")
@@ -99,12 +125,13 @@ def test_evidence_only_for_its_config_and_build(tmp_path, monkeypatch):
 
 
 def test_committed_evidence_is_self_consistent():
-    """Every committed profiles/r02 trace/PMC summary names its configuration and
+    """Every committed profiles/r0x trace/PMC summary names its configuration and
     build, and a bench line committed beside it quotes the same kernel time within 2 %."""
-    d = os.path.join(ROOT, "profiles", "r02")
-    if not os.path.isdir(d):
-        pytest.skip("no round-2 profiles yet")
-    for f in sorted(os.listdir(d)):
+    dirs = [os.path.join(ROOT, "profiles", r) for r in ("r02", "r03")]
+    files = [(d, f) for d in dirs if os.path.isdir(d) for f in sorted(os.listdir(d))]
+    if not files:
+        pytest.skip("no profiles yet")
+    for d, f in files:
         if f.startswith(("trace_", "pmc_")) and f.endswith(".json"):
             j = json.load(open(os.path.join(d, f)))
             assert "config" in j and "lib_hash" in j, f
@@ -132,7 +159,7 @@ def test_gpu_bench_lane_change_line():
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["config"]["kkt_dim"] == 140 and d["n_gpus"] == 1
     assert d["value"] > 0 and 0 < d["roofline"]["frac"] < 1
-    assert d["cpu_baseline"]["status_match"] is True
+    assert d["parity"]["pass"] is True and d["parity"]["instances"] == 64
 
 
 @pytest.mark.gpu
@@ -146,3 +173,5 @@ def test_gpu_bench_c3_small_line():
     assert d["success_rate"] == 1.0 and d["host_api"]["median_solves_per_s"] > 0
     assert d["cpu_baseline"]["cores"] == d["cpu_baseline"]["nproc"]
     assert d["summary_statistics"]["ip"]["success_rate"] == 1.0
+    assert d["parity"]["pass"] is True and d["parity"]["instances"] == 256
+    assert d["parity_fixtures"]["pass"] is True and d["parity_fixtures"]["files"] >= 10

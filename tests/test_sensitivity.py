@@ -136,7 +136,7 @@ def test_abi_sensitivity_argument_errors():
     from mcp_amd._lib import lib
 
     L = lib()
-    big = _abi.Desc(0, 40, 16, 0, 1, _abi.theta_dim(0, 40, 16))  # n + 2m = 72 > 64
+    big = _abi.Desc(0, 400, 200, 0, 1, _abi.theta_dim(0, 400, 200))  # n + 2m = 800 > MCPX_MAX_WG_KKT_DIM
     buf = np.zeros(8192)
     ptr = buf.ctypes.data
     assert L.mcpx_vjp_batch(C.byref(big), ptr, ptr, ptr, ptr, None, None, None, 1, ptr, None) == \
@@ -146,8 +146,11 @@ def test_abi_sensitivity_argument_errors():
     ok = _abi.Desc(0, 2, 2, 0, 1, _abi.theta_dim(0, 2, 2))
     assert L.mcpx_jvp_batch(C.byref(ok), ptr, ptr, ptr, ptr, -1, ptr, 1, ptr, None) == _abi.MCPX_EINVAL
     assert L.mcpx_vjp_batch(C.byref(ok), ptr, None, ptr, ptr, None, None, None, 1, ptr, None) == _abi.MCPX_EINVAL
-    if L.mcpx_device_count() == 0:  # no CPU fallback
+    if L.mcpx_device_count() == 0:  # no CPU fallback, for the one-wave and the workgroup kernels alike
         assert L.mcpx_vjp_batch(C.byref(ok), ptr, ptr, ptr, ptr, None, None, None, 1, ptr, None) == \
+            _abi.MCPX_ENODEV
+        wg = _abi.Desc(0, 40, 16, 0, 1, _abi.theta_dim(0, 40, 16))  # n + 2m = 72: workgroup kernels
+        assert L.mcpx_vjp_batch(C.byref(wg), ptr, ptr, ptr, ptr, None, None, None, 1, ptr, None) == \
             _abi.MCPX_ENODEV
         assert L.mcpx_jvp_batch(C.byref(ok), ptr, ptr, ptr, ptr, 1, ptr, 1, ptr, None) == _abi.MCPX_ENODEV
 
