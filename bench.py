@@ -206,6 +206,9 @@ def parse(argv=None):
     ap.add_argument("--sens", action="store_true",
                     help="BASELINE C5: each step is the batched solve + the rrule pullback (VJP kernel) of "
                          "f = Σx² + Σy² (src/AutoDiff.jl:42-82, test/runtests.jl:72-75)")
+    ap.add_argument("--unfused", action="store_true",
+                    help="with --sens: solve and pullback as two calls (solve, torch cotangent, "
+                         "mcpx_vjp_batch_device) instead of mcpx_solve_vjp_batch_device")
     ap.add_argument("--gather", action="store_true",
                     help="run the RCCL result collection even at world size 1 (rehearsal under torchrun)")
     ap.add_argument("--lane-change", type=int, default=0, metavar="T",
@@ -505,13 +508,13 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     gather = Gatherer(packed) if distributed else None
     stream = torch.cuda.current_stream(dev)
 
+    fused = a.sens and not a.unfused
     if a.sens:
-        from mcp_amd.batch import vjp_batch_device
+        from mcp_amd.batch import solve_vjp_batch_device, vjp_batch_device
 
         p = theta.shape[1]
         dtheta = torch.empty(B, p, dtype=torch.float64, device=dev)
         vstat = torch.empty(B, dtype=torch.int32, device=dev)
-        zeros_m = torch.zeros(B, m, dtype=torch.float64, device=dev)
         gx = torch.empty(B, n, dtype=torch.float64, device=dev)
         gy = torch.empty(B, m, dtype=torch.float64, device=dev)
 
@@ -519,16 +522,19 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         # cotangent of f = Σx² + Σy² (test/runtests.jl:72-75): ∂x = 2x, ∂y = 2y, ∂s = 0
         torch.mul(out["x"], 2.0, out=gx)
         torch.mul(out["y"], 2.0, out=gy)
-        vjp_batch_device(0, n, m, theta, out["x"], out["y"], out["s"], gx, gy, zeros_m, dtheta, vstat,
-                         stream=stream)
+        vjp_batch_device(0, n, m, theta, out["x"], out["y"], out["s"], gx, gy, None, dtheta, vstat, stream=stream)
 
     def step(evs):
         if evs:
             evs[0][0].record(stream)
-        solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
+        if fused:  # one call: the pullback runs in the solve kernel's epilogue
+            solve_vjp_batch_device(0, n, m, theta, out, ct=(2.0, 2.0, 0.0), dtheta=dtheta, status=vstat,
+                                   tol=a.tol, linear_solver=a.linear_solver, stream=stream)
+        else:
+            solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
         if evs:
             evs[0][1].record(stream)
-        if a.sens:
+        if a.sens and not fused:
             if evs:
                 evs[1][0].record(stream)
             pullback()
@@ -537,9 +543,9 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         if gather is not None:
             gather()
 
-    elapsed, ms = timed_steps(step, a, stream, world, dist, dev, 2 if a.sens else 1)
+    elapsed, ms = timed_steps(step, a, stream, world, dist, dev, 2 if (a.sens and not fused) else 1)
     kern_ms = float(np.mean(ms[0]))
-    vjp_ms = float(np.mean(ms[1])) if a.sens else 0.0
+    vjp_ms = float(np.mean(ms[1])) if (a.sens and not fused) else 0.0
     step_s = [sum(t) * 1e-3 for t in zip(*ms)]  # per-step device time of the solve (+ pullback)
     # PCIe-inclusive rate of the host-buffer API (mcpx_solve_batch: H→D θ, solve, D→H
     # results), median of --host-runs runs after one warm-up;
@@ -620,7 +626,9 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         "config": {"workload": (f"BASELINE {'C5' if a.sens else ('C2' if (n, m) == (16, 8) else 'C3')}: random dense "
                                 f"QP-KKT n={n} m={m} (KKT dim {N}), "
                                 f"fp64, global batch {G} ({B} on rank 0), tol={a.tol:g}"
-                                + (", solve + rrule pullback (VJP kernel) of f = Σx²+Σy²" if a.sens else "")),
+                                + ((", solve + rrule pullback of f = Σx²+Σy² "
+                                    + ("fused in one kernel" if fused else "(solve, then VJP kernel)"))
+                                   if a.sens else "")),
                    "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "solve_dim": NS,
                    "batch_per_gpu": B, "global_batch": G, "sparsity": a.sparsity,
                    "parallelism": f"dp{world} (instance shards, RCCL all-gather of results)" if distributed
@@ -632,11 +640,19 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         "host_api": host,
         "evidence": evidence_id(key, cfg),
     }
-    if a.sens:
+    if fused:
+        res["sensitivity"] = {
+            "fused": True, "solve_vjp_kernel_ms": kern_ms, "solve_vjp_per_s": B / (kern_ms * 1e-3),
+            "vjp_failed": int((vstat != 0).sum().item()),
+            "note": "mcpx_solve_vjp_batch_device: the rrule pullback of f = Σx²+Σy² runs in the epilogue of the "
+                    "SCHUR solve kernel (csrc/ipm_inst_fused.hip), one launch pair for solve + VJP; roofline = "
+                    "the solve's Newton-step FLOPs over the fused launch (the pullback's one LU per instance "
+                    "is not counted); --unfused times the two-call path"}
+    elif a.sens:
         vbytes = B * 8 * (2 * p + 3 * N + 2 * N)  # θ read, ∂θ written, (x,y,s) + cotangents read
         vflops = B * lu_flops(N)
         vexec = B * lu_flops(n + m)
-        res["sensitivity"] = {
+        res["sensitivity"] = {"fused": False,
             "vjp_kernel_ms": vjp_ms, "solve_kernel_ms": kern_ms, "vjp_per_s": B / (vjp_ms * 1e-3),
             "vjp_failed": int((vstat != 0).sum().item()),
             "vjp_roofline": {"flops_per_launch": vflops, "achieved_tflops": vflops / (vjp_ms * 1e-3) / 1e12,
@@ -665,8 +681,7 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         if a.sens:  # the pullback of the same instances against oracle_vjp_batch
             kv = min(k, 1024)
             x, y, s_ = (out[f][:kv].cpu().numpy() for f in ("x", "y", "s"))
-            rd, rs = coracle.vjp_batch(0, n, m, theta_host[:kv], x, y, s_, 2.0 * x, 2.0 * y, np.zeros_like(y),
-                                       nthreads=th)
+            rd, rs = coracle.vjp_batch(0, n, m, theta_host[:kv], x, y, s_, 2.0 * x, 2.0 * y, None, nthreads=th)
             res["parity"]["vjp"] = parity_report({"dtheta": dtheta[:kv].cpu().numpy(), "status": vstat[:kv].cpu().numpy()},
                                                  {"dtheta": rd, "status": rs}, ("dtheta", "status"), kv,
                                                  "oracle_vjp_batch on the GPU's solutions")

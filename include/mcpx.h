@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MCPX_VERSION 10400 /* 1.4.0 */
+#define MCPX_VERSION 10500 /* 1.5.0 */
 
 /* error codes */
 #define MCPX_OK 0
@@ -232,6 +232,33 @@ int mcpx_vjp_batch(const mcpx_desc* desc, const double* theta, const double* x, 
 int mcpx_vjp_batch_device(const mcpx_desc* desc, const double* theta, const double* x,
                           const double* y, const double* s, const double* gx, const double* gy,
                           const double* gs, double* dtheta, int32_t* status, void* stream);
+
+/* Solve and pullback in one call — the rrule of solve (src/AutoDiff.jl:42-82) applied
+ * at the returned iterate, for a loss whose cotangent is given per block as
+ *     ∂l/∂x = ax·x + bx,  ∂l/∂y = ay·y + by,  ∂l/∂s = as·s + bs
+ * (b arrays [B*n] / [B*m] on the device, NULL = 0; a = 0 with b = NULL is
+ * ChainRulesCore's ZeroTangent; a·z + b is rounded twice, no fma).  The AD test's
+ * f = Σx² + Σy² (test/runtests.jl:72-75) is {ax = 2, ay = 2, as = 0, NULLs}. */
+typedef struct mcpx_cotangent {
+  double ax, ay, as;
+  const double* bx; /* [B*n] or NULL */
+  const double* by; /* [B*m] or NULL */
+  const double* bs; /* [B*m] or NULL */
+} mcpx_cotangent;
+
+/* mcpx_solve_batch_device into `out`, then the pullback of `ct` at the solution into
+ * dtheta [B*p] / vjp_status [B] (or NULL), device buffers of the current device,
+ * enqueued on `stream`.  For the QP family with linear_solver = SCHUR at the
+ * compiled (n, m) of the benchmarks ((2,2), (16,8), (32,16)) the pullback runs in
+ * the epilogue of the solve kernel (one launch, the iterate never leaves the wave);
+ * every other configuration runs the solve and mcpx_vjp_batch_device on `stream`.
+ * Both give the bits of mcpx_solve_batch_device followed by mcpx_vjp_batch_device
+ * with gx = ax·x + bx, gy = ay·y + by, gs = as·s + bs. */
+int mcpx_solve_vjp_batch_device(const mcpx_desc* desc, const double* theta,
+                                const double* x0, const double* y0, const double* s0,
+                                const mcpx_params* prm, const mcpx_out* out,
+                                const mcpx_cotangent* ct, double* dtheta,
+                                int32_t* vjp_status, void* stream);
 
 /* Forward mode — the ForwardDiff.Dual method of solve (src/AutoDiff.jl:84-117):
  *     ż_c = (∂z/∂θ) θ̇_c = −(∇F_z)⁻¹ (∇F_θ θ̇_c),   c = 0 .. n_partials−1.

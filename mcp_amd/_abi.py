@@ -82,6 +82,18 @@ class Out(C.Structure):
     ]
 
 
+class Cotangent(C.Structure):
+    """mcpx_cotangent: ∂l/∂z = a·z + b per block (b device arrays or NULL)."""
+    _fields_ = [
+        ("ax", C.c_double),
+        ("ay", C.c_double),
+        ("as_", C.c_double),
+        ("bx", C.c_void_p),
+        ("by", C.c_void_p),
+        ("bs", C.c_void_p),
+    ]
+
+
 def make_params(tol=1e-4, max_inner_iters=20, max_outer_iters=50, tightening_rate=0.1,
                 loosening_rate=0.5, min_stepsize=1e-4, tau=0.995, decay=0.5,
                 linear_solver="reduced", kernel="auto") -> Params:

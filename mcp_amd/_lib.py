@@ -30,7 +30,7 @@ EXPORTS = ("mcpx_version", "mcpx_last_error", "mcpx_default_params", "mcpx_theta
            "mcpx_vjp_batch_device", "mcpx_jvp_batch", "mcpx_jvp_batch_device", "mcpx_module_load",
            "mcpx_module_dims", "mcpx_module_unload", "mcpx_solve_batch_module", "mcpx_solve_batch_module_device",
            "mcpx_host_register", "mcpx_host_unregister", "mcpx_vjp_batch_module", "mcpx_vjp_batch_module_device",
-           "mcpx_jvp_batch_module", "mcpx_jvp_batch_module_device")
+           "mcpx_jvp_batch_module", "mcpx_jvp_batch_module_device", "mcpx_solve_vjp_batch_device")
 
 
 def lib():
@@ -64,6 +64,9 @@ def lib():
     L.mcpx_jvp_batch.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, C.c_int, P, P]
     L.mcpx_jvp_batch_device.restype = C.c_int
     L.mcpx_jvp_batch_device.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, P, P, P]
+    L.mcpx_solve_vjp_batch_device.restype = C.c_int
+    L.mcpx_solve_vjp_batch_device.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, C.POINTER(_abi.Params),
+                                              C.POINTER(_abi.Out), C.POINTER(_abi.Cotangent), P, P, C.c_void_p]
     I32P = C.POINTER(C.c_int32)
     L.mcpx_module_load.restype = C.c_int
     L.mcpx_module_load.argtypes = [C.c_char_p, C.POINTER(C.c_void_p)]

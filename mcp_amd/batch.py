@@ -279,6 +279,46 @@ def vjp_batch_device(family: int, n: int, m: int, theta, x, y, s, gx=None, gy=No
     return dtheta, status
 
 
+def solve_vjp_batch_device(family: int, n: int, m: int, theta, out: dict | None = None, *, ct=(0.0, 0.0, 0.0),
+                           bx=None, by=None, bs=None, dtheta=None, status=None, x0=None, y0=None, s0=None,
+                           params=None, stream=None, **kw):
+    """Solve and pull back in one call (mcpx_solve_vjp_batch_device): the solve into
+    `out` (as :func:`solve_batch_device`), then ∂θ of the loss whose cotangent is
+    ∂l/∂x = ct[0]·x + bx, ∂l/∂y = ct[1]·y + by, ∂l/∂s = ct[2]·s + bs (b tensors or
+    None = 0).  The README / C5 loss f = Σx² + Σy² is ct = (2, 2, 0).  SCHUR QPs at the
+    benchmark sizes run the pullback inside the solve kernel.  Returns
+    (out, dtheta (B, p), status (B,))."""
+    import torch
+
+    if not (theta.is_cuda and theta.dtype == torch.float64 and theta.dim() == 2 and theta.is_contiguous()):
+        raise ValueError("theta must be a contiguous (B, p) float64 device tensor")
+    B, ld = theta.shape
+    dev = theta.device
+    if out is None:
+        out = alloc_device_outputs(B, n, m, dev)
+    if dtheta is None:
+        dtheta = torch.empty(B, _abi.theta_dim(family, n, m), dtype=torch.float64, device=dev)
+    if status is None:
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+    for t in (x0, y0, s0):
+        if t is not None and not (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()):
+            raise ValueError("warm starts must be contiguous float64 device tensors")
+    dp = lambda t: None if t is None else t.data_ptr()
+    tl = 0 if out.get("alpha_trace") is None else out["alpha_trace"].shape[1]
+    o = _abi.Out(dp(out["x"]), dp(out["y"]), dp(out["s"]), dp(out["kkt_error"]), dp(out["eps"]),
+                 dp(out["outer_iters"]), dp(out["status"]), dp(out.get("newton_iters")),
+                 dp(out.get("active_mask")), dp(out.get("alpha_trace")), int(tl), 0)
+    cot = _abi.Cotangent(float(ct[0]), float(ct[1]), float(ct[2]), _dev_f64(bx, "bx"), _dev_f64(by, "by"),
+                         _dev_f64(bs, "bs"))
+    prm = _params(params, **kw)
+    desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    check(lib().mcpx_solve_vjp_batch_device(C.byref(desc), dp(theta), dp(x0), dp(y0), dp(s0), C.byref(prm),
+                                            C.byref(o), C.byref(cot), _dev_f64(dtheta, "dtheta"), dp(status),
+                                            C.c_void_p(st.cuda_stream)))
+    return out, dtheta, status
+
+
 def jvp_batch_device(family: int, n: int, m: int, theta, x, y, s, theta_dot, zdot=None, status=None,
                      stream=None, module: Module | None = None):
     """Device-tensor tangents: theta_dot (B, K, p) → (zdot (B, K, n+2m), status (B,))."""

@@ -13,6 +13,7 @@ from __future__ import annotations
 import glob
 import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -26,7 +27,7 @@ LIB = os.path.join(HERE, "libmcpx.so")
 SOURCES = [os.path.join(CSRC, f) for f in (
     "ipm_inst_red_qp.hip", "ipm_inst_spec.hip", "ipm_inst_schur_qp.hip", "ipm_inst_red_aff.hip",
     "ipm_inst_dense_qp.hip", "ipm_inst_dense_aff.hip", "sens_inst_vjp.hip", "sens_inst_jvp.hip",
-    "ipm_inst_wg.hip", "sens_inst_wg.hip", "mcpx_api.cpp")]
+    "ipm_inst_wg.hip", "sens_inst_wg.hip", "ipm_inst_fused.hip", "mcpx_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("ipm_kernel.h", "ipm_kernel_impl.hpp", "bcast_group.inc", "sens_kernel.h", "sens_kernel_impl.hpp",
     "ipm_wg.h", "ipm_wg_impl.hpp", "sens_wg_impl.hpp")] + [
     os.path.join(ROOT, "include", "mcpx.h")]
@@ -66,6 +67,27 @@ def _stale() -> bool:
     return not os.path.exists(LIB) or built_hash() != source_hash()
 
 
+# Per-translation-unit object cache of this container (never shipped): a TU is recompiled
+# only when its text, a file it includes (transitively) or the flags change.
+OBJ_CACHE = os.environ.get("MCPX_OBJ_CACHE") or os.path.join(os.path.expanduser("~"), ".cache", "mcpx_objs")
+_INCLUDE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _tu_key(src: str, flags) -> str:
+    h = hashlib.sha256(" ".join([HIPCC, *flags]).encode())
+    seen, todo = set(), [os.path.abspath(src)]
+    while todo:
+        f = todo.pop()
+        if f in seen or not os.path.exists(f):
+            continue
+        seen.add(f)
+        text = open(f, "rb").read()
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0" + text + b"\0")
+        todo += [os.path.normpath(os.path.join(os.path.dirname(f), inc))
+                 for inc in _INCLUDE.findall(text.decode(errors="replace"))]
+    return h.hexdigest()[:24]
+
+
 def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str | None = None) -> str:
     """`out`: alternative output path (kernel A/B variants built with `extra_flags`)."""
     lib_path = out or LIB
@@ -75,19 +97,41 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     objs, procs = [], []
     jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 1)
     tmp_dir = tempfile.mkdtemp(prefix="mcpx_build_")
+    built = []  # (cache dir, tmp object) of the TUs compiled in this call
     for src in SOURCES:  # one hipcc per translation unit, `jobs` at a time
-        obj = os.path.join(tmp_dir, os.path.basename(src) + ".o")
+        base = os.path.basename(src)
+        obj = os.path.join(tmp_dir, base + ".o")
+        cdir = os.path.join(OBJ_CACHE, base + "." + _tu_key(src, [*FLAGS, *extra_flags]))
+        objs.append(obj)
+        if not force and os.path.exists(os.path.join(cdir, "ok")):  # object + device .s of an identical TU
+            for f in os.listdir(cdir):
+                if f != "ok":
+                    shutil.copy2(os.path.join(cdir, f), os.path.join(tmp_dir, f))
+            if verbose:
+                print(f"cached {base}", flush=True)
+            continue
         # -save-temps=obj keeps the device .s next to the object for the hazard check
         cmd = [HIPCC, *FLAGS, *extra_flags, "-save-temps=obj", "-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
-        procs.append(subprocess.Popen(cmd))
-        objs.append(obj)
-        while sum(p.poll() is None for p in procs) >= jobs:
+        procs.append((subprocess.Popen(cmd), src))
+        built.append((cdir, src))
+        while sum(p.poll() is None for p, _ in procs) >= jobs:
             time.sleep(0.2)
-    for p, src in zip(procs, SOURCES):
+    for p, src in procs:
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, f"hipcc {src}")
+    for cdir, src in built:
+        base = os.path.basename(src)
+        stem = os.path.splitext(base)[0]
+        try:
+            os.makedirs(cdir, exist_ok=True)
+            for f in os.listdir(tmp_dir):
+                if f == base + ".o" or (f.startswith(stem + "-hip-amdgcn") and f.endswith(".s")):
+                    shutil.copy2(os.path.join(tmp_dir, f), os.path.join(cdir, f))
+            open(os.path.join(cdir, "ok"), "w").close()
+        except OSError:
+            pass  # the cache is an accelerator only
     # hipcc does not pad hazards whose reader sits inside inline asm: refuse a build in
     # which a compiler-placed VALU write feeds a DPP / cross-lane asm read too early
     checker = os.path.join(ROOT, "tools", "check_dpp_hazards.py")

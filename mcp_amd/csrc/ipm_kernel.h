@@ -41,6 +41,14 @@ struct KernelArgs {
   double decay;
   double tight[MCPX_MAX_INNER_ITERS + 1];  // 1 − exp(−t·k), src/solver.jl:112
   double loose[MCPX_MAX_INNER_ITERS + 1];  // 1 + exp(−l·k), src/solver.jl:113
+  // fused rrule pullback (mcpx_solve_vjp_batch_device, the FUSE kernels only): ∂θ of the
+  // instance right after its solve, cotangent g = a ⊙ z + b (sens_kernel.h SensArgs)
+  double* vjp_dtheta;
+  int32_t* vjp_status;
+  const double* ct_bx;  // b of the x / y / s cotangent blocks, [B*n] / [B*m] / [B*m] or NULL = 0
+  const double* ct_by;
+  const double* ct_bs;
+  double ct_ax, ct_ay, ct_as;  // a (scalars)
 };
 
 // Launchers of the register-resident solver: one 64-lane wave (= one
@@ -54,5 +62,10 @@ hipError_t launch_ipm_red_qp(int nmax, const KernelArgs& a, int64_t batch, hipSt
 hipError_t launch_ipm_red_aff(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 hipError_t launch_ipm_dense_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 hipError_t launch_ipm_dense_aff(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
+// The SCHUR QP solve with the rrule pullback fused into its epilogue (ipm_inst_fused.hip):
+// compile-time (n, m) ∈ {(2, 2), (16, 8), (32, 16)}; hipErrorNotFound otherwise.
+hipError_t launch_ipm_fused_vjp(int family, int solver, int n, int m, const KernelArgs& a, int64_t batch,
+                                hipStream_t st);
+bool has_fused_vjp(int family, int solver, int n, int m);
 
 }  // namespace mcpx

@@ -56,6 +56,10 @@
 #ifndef MCPX_FAST_WAVES
 #define MCPX_FAST_WAVES 5
 #endif
+// … and in the fast pass with the fused pullback (its register row is n + m wide).
+#ifndef MCPX_FUSED_WAVES
+#define MCPX_FUSED_WAVES 4
+#endif
 
 // Diagnostic phase stamps (tools/phase_profile.hip builds with MCPX_STAMPS=1;
 // the product build compiles them away).
@@ -765,6 +769,12 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
   return true;
 }
 
+// The rrule pullback fused into the solve kernel's epilogue (defined in
+// sens_kernel_impl.hpp; only the FUSE instantiations of ipm_inst_fused.hip use it).
+template <int NV, int FAMILY>
+__device__ __forceinline__ void fused_vjp(const KernelArgs& A, int64_t inst, int ln, int n, int m, double z, double s,
+                          const double* th);
+
 }  // namespace
 
 // v of lane `src` (ds_bpermute through the LDS crossbar; no LDS allocation).
@@ -807,8 +817,10 @@ __device__ __forceinline__ void schur_rows_from_2d(const d4 (&acc)[NT][NT], int 
 //      again from the start with every path compiled in (the computation is
 //      deterministic, so they end bit-identical to a single complete pass); all
 //      others exit at once.
-template <int NMAX, int FAMILY, int NC, int MC, int SOLVER, int PASS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? MCPX_FAST_WAVES : 1, 8))) void ipm_solve_kernel(const KernelArgs args) {
+// FUSE > 0 (ipm_inst_fused.hip): the instance's rrule pullback runs in the epilogue
+// (fused_vjp, register width FUSE ≥ n + m) once its solve is final — mcpx_solve_vjp_batch_device.
+template <int NMAX, int FAMILY, int NC, int MC, int SOLVER, int PASS, int FUSE = 0>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? (FUSE > 0 ? MCPX_FUSED_WAVES : MCPX_FAST_WAVES) : 1, 8))) void ipm_solve_kernel(const KernelArgs args) {
   constexpr bool RED = SOLVER != MCPX_LINSOLVE_DENSE;  // lanes [0,n) x, [n,n+m) (y, s)
   constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR;
   static_assert(SCH || PASS == 0, "two-pass launch is for the SCHUR solver only");
@@ -1093,18 +1105,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
     args.status[inst] = status;
     if (args.newton_iters) args.newton_iters[inst] = newton;
   }
+  if constexpr (FUSE > 0) {
+    static_assert(RED && FAMILY == MCPX_FAMILY_QP, "the fused pullback follows the QP REDUCED / SCHUR lane layout");
+    fused_vjp<FUSE, FAMILY>(args, inst, lane, n, m, z, s, th0);
+  }
 }
 
 // Launch helper used by the instantiation units.
-template <int NMAX, int FAMILY, int NC, int MC, int SOLVER>
+template <int NMAX, int FAMILY, int NC, int MC, int SOLVER, int FUSE = 0>
 hipError_t launch_one(const KernelArgs& args, int64_t batch, hipStream_t stream) {
   if constexpr (SOLVER == MCPX_LINSOLVE_SCHUR) {  // fast pass, then the deferred instances
-    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 1>), dim3((unsigned)batch), dim3(64), 0,
+    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 1, FUSE>), dim3((unsigned)batch), dim3(64), 0,
                        stream, args);
-    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 2>), dim3((unsigned)batch), dim3(64), 0,
+    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 2, FUSE>), dim3((unsigned)batch), dim3(64), 0,
                        stream, args);
   } else {
-    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 0>), dim3((unsigned)batch), dim3(64), 0,
+    hipLaunchKernelGGL((ipm_solve_kernel<NMAX, FAMILY, NC, MC, SOLVER, 0, FUSE>), dim3((unsigned)batch), dim3(64), 0,
                        stream, args);
   }
   return hipGetLastError();

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -57,12 +58,23 @@ int fail(int code, const char* fmt, ...) {
   } while (0)
 
 int check_device(int dev) {
+  static std::atomic<uint64_t> verified{0};  // devices already found to be gfx950 (bit per ordinal < 64)
+  if (dev >= 0 && dev < 64 && ((verified.load(std::memory_order_relaxed) >> dev) & 1)) return MCPX_OK;
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, dev));
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return fail(MCPX_ENODEV, "device %d is %s; this build targets gfx950 (MI355X) only", dev,
                 prop.gcnArchName);
+  if (dev >= 0 && dev < 64) verified.fetch_or(uint64_t(1) << dev, std::memory_order_relaxed);
   return MCPX_OK;
+}
+
+// The current device of a device-buffer call: MCPX_ENODEV when none is visible.
+int current_device(int* dev) {
+  const hipError_t e = hipGetDevice(dev);
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return fail(MCPX_ENODEV, "no HIP device visible");
+  HIP_TRY(e);
+  return check_device(*dev);
 }
 
 // MCPX_GENERIC_KERNELS=1 disables the compile-time-(n, m) kernels (A/B switch).
@@ -832,8 +844,7 @@ int vjp_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, c
   if (d->batch == 0) return MCPX_OK;
   if ((rc = sens_inputs_ok(d, theta, x, y, s, dtheta))) return rc;
   int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if ((rc = check_device(dev))) return rc;
+  if ((rc = current_device(&dev))) return rc;
   return launch_sens(false, d, a, plan, theta, x ? x : theta, y ? y : theta, s ? s : theta, gx, gy, gs, nullptr,
                      dtheta, status, (hipStream_t)stream);
 }
@@ -863,8 +874,7 @@ int jvp_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, c
   if ((rc = sens_inputs_ok(d, theta, x, y, s, zdot))) return rc;
   if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
   int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if ((rc = check_device(dev))) return rc;
+  if ((rc = current_device(&dev))) return rc;
   return launch_sens(true, d, a, plan, theta, x ? x : theta, y ? y : theta, s ? s : theta, nullptr, nullptr,
                      nullptr, theta_dot, zdot, status, (hipStream_t)stream);
 }
@@ -899,9 +909,54 @@ int solve_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta,
   if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
   if (o->active_mask && d->m > 64) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
   int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if ((rc = check_device(dev))) return rc;
+  if ((rc = current_device(&dev))) return rc;
   return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod, wg);
+}
+
+// mcpx_solve_vjp_batch_device: the solve kernels with the pullback in their epilogue
+// (ipm_inst_fused.hip) where they exist, else the solve then the VJP launches.
+int solve_vjp_device_impl(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
+                          const double* s0, const mcpx_params* prm, const mcpx_out* o, const mcpx_cotangent* ct,
+                          double* dtheta, int32_t* vstat, void* stream) {
+  mcpx::KernelArgs a;
+  int nmax;
+  bool wg = false;
+  int rc = prepare(d, prm, &a, &nmax, nullptr, &wg);
+  if (rc) return rc;
+  mcpx::SensArgs sa;
+  SensPlan plan;
+  if ((rc = prepare_sens(d, &sa, &plan, false))) return rc;
+  if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
+  if (!ct) return fail(MCPX_EINVAL, "the cotangent must be non-NULL");
+  if (d->batch == 0) return MCPX_OK;
+  if (!theta || !dtheta) return fail(MCPX_EINVAL, "theta and dtheta must be non-NULL");
+  if (o->active_mask && d->m > 64) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
+  int dev = 0;
+  if ((rc = current_device(&dev))) return rc;
+  const hipStream_t st = (hipStream_t)stream;
+  const int n = d->n, m = d->m;
+  if (!wg && specialized_enabled() && mcpx::has_fused_vjp(a.family, a.solver, n, m)) {
+    const int64_t CH = (int64_t)1 << 30;
+    a.ct_ax = ct->ax;
+    a.ct_ay = ct->ay;
+    a.ct_as = ct->as;
+    for (int64_t b0 = 0; b0 < d->batch; b0 += CH) {
+      const int64_t nb = std::min(CH, d->batch - b0);
+      set_chunk(a, d, theta, x0, y0, s0, o, b0);
+      a.vjp_dtheta = dtheta + b0 * sa.p;
+      a.vjp_status = vstat ? vstat + b0 : nullptr;
+      a.ct_bx = ct->bx ? ct->bx + b0 * n : nullptr;
+      a.ct_by = ct->by ? ct->by + b0 * m : nullptr;
+      a.ct_bs = ct->bs ? ct->bs + b0 * m : nullptr;
+      HIP_TRY(mcpx::launch_ipm_fused_vjp(a.family, a.solver, n, m, a, nb, st));
+    }
+    return MCPX_OK;
+  }
+  if ((rc = launch_chunks(d, theta, x0, y0, s0, o, a, nmax, st, nullptr, wg))) return rc;
+  sa.ga_x = ct->ax;
+  sa.ga_y = ct->ay;
+  sa.ga_s = ct->as;
+  return launch_sens(false, d, sa, plan, theta, o->x, o->y, o->s, ct->bx, ct->by, ct->bs, nullptr, dtheta, vstat, st);
 }
 
 // mcpx_solve_batch / mcpx_solve_batch_module: contiguous shards, one host thread per device.
@@ -976,6 +1031,12 @@ int mcpx_device_count(void) {
 int mcpx_solve_batch_device(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                             const double* s0, const mcpx_params* prm, const mcpx_out* o, void* stream) {
   return solve_device_impl(nullptr, d, theta, x0, y0, s0, prm, o, stream);
+}
+
+int mcpx_solve_vjp_batch_device(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
+                                const double* s0, const mcpx_params* prm, const mcpx_out* out,
+                                const mcpx_cotangent* ct, double* dtheta, int32_t* vjp_status, void* stream) {
+  return solve_vjp_device_impl(d, theta, x0, y0, s0, prm, out, ct, dtheta, vjp_status, stream);
 }
 
 int mcpx_solve_batch(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,

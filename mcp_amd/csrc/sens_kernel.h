@@ -26,7 +26,18 @@ struct SensArgs {
   int32_t n, m;
   int32_t n_partials;       // K (JVP)
   int32_t family;
+  // VJP cotangent g = a ⊙ z + b per block (b = gx / gy / gs above, NULL = 0): a = 0 is the
+  // plain cotangent arrays; a ≠ 0 the gradient of a separable quadratic loss
+  // l = Σ ½ a z² + b·z (e.g. a = 2, b = 0: f = Σx² + Σy², test/runtests.jl:72-75),
+  // computed in the kernel as a·z + b (two roundings, no fma)
+  double ga_x, ga_y, ga_s;
 };
+
+// One cotangent entry g = a·z + b (a = 0 → b, 0 when b is absent; b absent → a·z).
+__device__ __forceinline__ double affine_ct(double a, double z, const double* b) {
+  if (a == 0.0) return b ? *b : 0.0;
+  return b ? a * z + *b : a * z;
+}
 
 // One 64-lane wave per instance; nmax ∈ {8,16,24,32,48,64} ≥ n + 2m.
 // hipErrorInvalidValue when no kernel matches.

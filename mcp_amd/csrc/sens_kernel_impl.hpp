@@ -301,21 +301,15 @@ __device__ __forceinline__ void vjp_reduced_row(const double* __restrict__ th, c
     for (int k = 0; k < m; ++k) rhs = fma(ph[k * sh], gsv[k], rhs);
 }
 
+// The pullback of one instance (the rrule of src/AutoDiff.jl:42-82), one wave: zs = z =
+// [x; y; s] in LDS, `lam` LDS scratch (≥ n+m), g = this lane's cotangent entry of the x / y
+// rows, gsv = the s block's cotangent (any address space) or NULL = zero.  Writes ∂θ
+// (family layout, stride p) to `o` and 0 / 1 (∇F_z singular) to *st.
 template <int NMAX, int FAMILY>
-__global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
-  __shared__ double zs[64];
-  __shared__ double lam[64];
-  const int ln = threadIdx.x;
-  const int64_t inst = blockIdx.x;
-  const int n = A.n, m = A.m, N = n + 2 * m;
-  const double* th = A.theta + inst * A.theta_ld;
-  load_z(A, inst, ln, zs);
-  __syncthreads();
+__device__ __forceinline__ void vjp_instance(const double* __restrict__ th, const double* zs, double* lam,
+                                             const double* gsv, double g, int ln, int n, int m, double* __restrict__ o,
+                                             int32_t* st) {
   double a[NMAX];
-  double g = 0.0;  // ∂l/∂z_ln (NULL cotangent block = ZeroTangent)
-  if (ln < n) { if (A.gx) g = A.gx[inst * n + ln]; }
-  else if (ln < n + m) { if (A.gy) g = A.gy[inst * m + (ln - n)]; }
-  const double* gsv = A.gs ? A.gs + inst * m : nullptr;
   vjp_reduced_row<NMAX, FAMILY>(th, zs, gsv, ln, n, m, a, g);
   double l = 0.0;
   const bool ok = lu_solve_rows<NMAX>(a, g, n + m, ln, l);
@@ -327,9 +321,7 @@ __global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
   }
   lam[ln] = ok ? lv : __builtin_nan("");
   __syncthreads();
-  (void)N;
-  if (A.status && ln == 0) A.status[inst] = ok ? 0 : 1;
-  double* o = A.out + inst * A.p;
+  if (st && ln == 0) *st = ok ? 0 : 1;
   const int64_t nn = (int64_t)n * n, nm = (int64_t)n * m, mm = (int64_t)m * m;
   const double* x = zs;
   const double* y = zs + n;
@@ -348,6 +340,57 @@ __global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
     write_block(o + nn + 2 * nm + mm, n, 1, ln, [&](int i, int) { return -lx[i]; });       // ∂g_i
     write_block(o + nn + 2 * nm + mm + n, m, 1, ln, [&](int k, int) { return -ly[k]; });   // ∂h_k
   }
+}
+
+template <int NMAX, int FAMILY>
+__global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
+  __shared__ double zs[64];
+  __shared__ double lam[64];
+  __shared__ double gsl[64];
+  const int ln = threadIdx.x;
+  const int64_t inst = blockIdx.x;
+  const int n = A.n, m = A.m;
+  const double* th = A.theta + inst * A.theta_ld;
+  load_z(A, inst, ln, zs);
+  __syncthreads();
+  // ∂l/∂z_ln of the x / y rows (NULL block with a = 0: ZeroTangent)
+  double g = 0.0;
+  if (ln < n) g = affine_ct(A.ga_x, zs[ln], A.gx ? A.gx + inst * n + ln : nullptr);
+  else if (ln < n + m) g = affine_ct(A.ga_y, zs[ln], A.gy ? A.gy + inst * m + (ln - n) : nullptr);
+  const double* gsv = A.gs ? A.gs + inst * m : nullptr;
+  if (A.ga_s != 0.0) {  // the s block's cotangent a·s + b, materialised for the row chains
+    if (ln < m) gsl[ln] = affine_ct(A.ga_s, zs[n + m + ln], A.gs ? A.gs + inst * m + ln : nullptr);
+    __syncthreads();
+    gsv = gsl;
+  }
+  vjp_instance<NMAX, FAMILY>(th, zs, lam, gsv, g, ln, n, m, A.out + inst * A.p, A.status ? A.status + inst : nullptr);
+}
+
+// The pullback fused into the solve kernel's epilogue (ipm_solve_kernel<…, FUSE = NV>):
+// the solve's lane layout (lanes [0, n) x, [n, n+m) y with s in `s`) into LDS, the
+// cotangent a ⊙ z + b of KernelArgs, vjp_instance with register width NV ≥ n + m.
+template <int NV, int FAMILY>
+__device__ __forceinline__ void fused_vjp(const KernelArgs& A, int64_t inst, int ln, int n, int m, double z, double s,
+                          const double* th) {
+  __shared__ double zs[64];
+  __shared__ double lam[64];
+  __shared__ double gsl[64];
+  __syncthreads();
+  if (ln < n + m) zs[ln] = z;
+  if (ln >= n && ln < n + m) zs[ln + m] = s;
+  __syncthreads();
+  double g = 0.0;
+  if (ln < n) g = affine_ct(A.ct_ax, zs[ln], A.ct_bx ? A.ct_bx + inst * n + ln : nullptr);
+  else if (ln < n + m) g = affine_ct(A.ct_ay, zs[ln], A.ct_by ? A.ct_by + inst * m + (ln - n) : nullptr);
+  const double* gsv = nullptr;
+  if (A.ct_as != 0.0 || A.ct_bs) {
+    if (ln < m) gsl[ln] = affine_ct(A.ct_as, zs[n + m + ln], A.ct_bs ? A.ct_bs + inst * m + ln : nullptr);
+    __syncthreads();
+    gsv = gsl;
+  }
+  const int64_t p = (int64_t)n * n + (int64_t)m * n + m + n;  // QP θ dimension (mcpx_theta_dim)
+  vjp_instance<NV, FAMILY>(th, zs, lam, gsv, g, ln, n, m, A.vjp_dtheta + inst * p,
+                           A.vjp_status ? A.vjp_status + inst : nullptr);
 }
 
 template <int NMAX, int FAMILY>

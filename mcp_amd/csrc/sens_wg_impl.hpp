@@ -144,6 +144,8 @@ __device__ __forceinline__ void sens_instances(const WgSensArgs& W) {
     __syncthreads();
     if (inst >= W.batch) break;  // every workgroup reaches this exit
     const double* __restrict__ th = a.theta + inst * a.theta_ld;
+    const bool has_gs = a.gs || a.ga_s != 0.0;  // else ∂l/∂s = ZeroTangent
+    auto gs_at = [&](int k) { return affine_ct(a.ga_s, zs[nr + k], a.gs ? a.gs + inst * m + k : nullptr); };
 
     // z = [x; y; s] at the returned iterate (src/AutoDiff.jl:25)
     for (int i = tid; i < N; i += WG)
@@ -182,11 +184,12 @@ __device__ __forceinline__ void sens_instances(const WgSensArgs& W) {
               const int k = j - n;
               v = qp_y ? 0.0 : jac<FAMILY, GEN>(th, blk, zs, n, m, n + k, r) * zs[n + k];  // ∇F_z[n+k][r]·y_k
               if (r == n + k) v = v + zs[nr + k];                                          // + s_k
-            } else {  // g_r + Σ_k ∇F_z[n+k][r]·gs_k, k ascending
-              double acc = r < n ? (a.gx ? a.gx[inst * n + r] : 0.0) : (a.gy ? a.gy[inst * m + (r - n)] : 0.0);
-              if (a.gs && !qp_y)
+            } else {  // g_r + Σ_k ∇F_z[n+k][r]·gs_k, k ascending (g = a ⊙ z + b, SensArgs ga_*)
+              double acc = r < n ? affine_ct(a.ga_x, zs[r], a.gx ? a.gx + inst * n + r : nullptr)
+                                 : affine_ct(a.ga_y, zs[r], a.gy ? a.gy + inst * m + (r - n) : nullptr);
+              if (has_gs && !qp_y)
                 for (int k = 0; k < m; ++k)
-                  acc = fma(jac<FAMILY, GEN>(th, blk, zs, n, m, n + k, r), a.gs[inst * m + k], acc);
+                  acc = fma(jac<FAMILY, GEN>(th, blk, zs, n, m, n + k, r), gs_at(k), acc);
               v = acc;
             }
           }
@@ -210,7 +213,7 @@ __device__ __forceinline__ void sens_instances(const WgSensArgs& W) {
         double u = xs[i];
         if (i >= n) {
           const int k = i - n;
-          u = a.gs ? fma(zs[n + k], u, -a.gs[inst * m + k]) : zs[n + k] * u;
+          u = has_gs ? fma(zs[n + k], u, -gs_at(k)) : zs[n + k] * u;
         }
         lam[i] = u;
       }
