@@ -66,6 +66,7 @@
 #ifndef MCPX_STAMPS
 #define MCPX_STAMPS 0
 #endif
+#define MCPX_NSTAMP 6  // residuals | ‖F‖∞ + rr | Schur form | LU / GJ | back-substitution | line search + update
 #if MCPX_STAMPS
 #define MCPX_STAMP(i)                                 \
   do {                                                \
@@ -670,12 +671,51 @@ __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, 
 // pivot row a_kj ← fma(a_kj, +0, a_kj), rh_k likewise; x_i = rh_i / a_ii).  Entries of columns ≤ k are also touched in a lane
 // whose local column block straddles k; those are never read again.
 // rh[J] / x[J]: row 16J + lc, replicated over the four DPP rows.
+// Gauss-Jordan knobs (A/B: profiles/r03/ab_c3_gj_bperm.jsonl, same bits either way):
+// MCPX_GJ_BPERM = 1 hands every lane its rows' pivot-column entries with ds_bpermute
+// (LDS crossbar: 2 LDS instructions and 1 product per row half, instead of the
+// 17-VALU permlane chain of col_quot_nt2 / from_dpp_row); MCPX_GJ_DGLANE = 1 records
+// pivot k in lane k (two v_writelane) instead of a compare-and-select per pivot.
+// C3 at 65,536: 13.1 → 15.0 M solves/s; a lone wave's step 10 % shorter.
+#ifndef MCPX_GJ_BPERM
+#define MCPX_GJ_BPERM 1
+#endif
+#ifndef MCPX_GJ_DGLANE
+#define MCPX_GJ_DGLANE 1
+#endif
+
+// v of the lane whose byte address (4 × lane) is `addr` (ds_bpermute, no LDS allocation).
+__device__ __forceinline__ double bperm_f64_addr(double v, int addr) {
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+// v with lane `k` replaced by the wave-uniform u (two v_writelane_b32; u in SGPRs, the
+// lane select an inline constant: k is static after the caller's unrolling).
+__device__ __forceinline__ double writelane_f64(double v, double u, int k) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  const int ulo = __builtin_amdgcn_readfirstlane(__double2loint(u));
+  const int uhi = __builtin_amdgcn_readfirstlane(__double2hiint(u));
+#define C(K) \
+  case K: asm volatile("v_writelane_b32 %0, %2, " #K "\n v_writelane_b32 %1, %3, " #K : "+v"(lo), "+v"(hi) : "s"(ulo), "s"(uhi)); break;
+  switch (k) { C(0) C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11) C(12) C(13) C(14) C(15) C(16) C(17) C(18) C(19) C(20) C(21) C(22) C(23) C(24) C(25) C(26) C(27) C(28) C(29) C(30) C(31) C(32) C(33) C(34) C(35) C(36) C(37) C(38) C(39) C(40) C(41) C(42) C(43) C(44) C(45) C(46) C(47) C(48) C(49) C(50) C(51) C(52) C(53) C(54) C(55) C(56) C(57) C(58) C(59) C(60) C(61) C(62) C(63)
+  }
+#undef C
+  return __hiloint2double(hi, lo);
+}
+
+// xo: the solution entry of row ln (lanes < N; lane 16J + lc is row 16J + lc).
 template <int NT, bool PAD>
-__device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[NT], int N, int ln, double (&x)[NT]) {
+__device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[NT], int N, int ln, double& xo) {
   const int lc = ln & 15;
   double dg[NT];
 #pragma unroll
   for (int J = 0; J < NT; ++J) dg[J] = 1.0;
+  double dgl = 1.0;  // MCPX_GJ_DGLANE: pivot k in lane k
+  int ad[4];         // MCPX_GJ_BPERM: byte address of lane 16·Q + lc
+#pragma unroll
+  for (int Q = 0; Q < 4; ++Q) ad[Q] = (16 * Q + lc) << 2;
   // A pivot that is not > 0 (not numerically SPD, or NaN) is only recorded: the
   // remaining steps run on (discarded) values instead of branching on every pivot,
   // which keeps the compare off the step's dependency chain.
@@ -690,9 +730,13 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
     bad |= !(piv > 0.0);
     const double rp = rcp_uniform(piv);  // oracle gj_spd_solve: l_i = a_ik · (1 / a_kk)
     const bool prow = lc == Rk;  // this lane holds the pivot row in half Jk
-    if (prow) dg[Jk] = piv;
+    if constexpr (MCPX_GJ_DGLANE) dgl = writelane_f64(dgl, piv, k);
+    else if (prow) dg[Jk] = piv;
     double nl[NT];
-    if constexpr (NT == 2) {
+    if constexpr (MCPX_GJ_BPERM) {  // column k: DPP row Qk of every half register
+#pragma unroll
+      for (int J = 0; J < NT; ++J) nl[J] = (-bperm_f64_addr(acc[Ik][J][rk], ad[Qk])) * rp;
+    } else if constexpr (NT == 2) {
       double q0, q1;  // −l of rows lc and 16 + lc: the fma takes −l · u exactly as fma(−l, u, a)
       switch (Qk + (k == 0 ? 4 : 0)) {  // static after unrolling
         case 0: col_quot_nt2<0, false>(acc[Ik][0][rk], acc[Ik][1][rk], rp, q0, q1); break;
@@ -764,8 +808,14 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
     }
   }
   if (bad) return false;
+  double r = rh[0], d = dg[0];
 #pragma unroll
-  for (int J = 0; J < NT; ++J) x[J] = rh[J] / dg[J];
+  for (int J = 1; J < NT; ++J)
+    if ((ln >> 4) == J) {
+      r = rh[J];
+      d = dg[J];
+    }
+  xo = r / (MCPX_GJ_DGLANE ? dgl : d);
   return true;
 }
 
@@ -898,7 +948,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   int outer = 1;                       // :70
   int newton = 0;
 #if MCPX_STAMPS
-  uint64_t st_acc[4] = {0, 0, 0, 0};
+  uint64_t st_acc[MCPX_NSTAMP] = {};
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -939,6 +989,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       } else {
         assemble_row<NMAX, FAMILY, RED, (NC > 0)>(th, zs, ln, n, m, eps, tol, s, a, F, Fc, rhs, w);
       }
+      MCPX_STAMP(0);
       // ‖F‖∞ with NaN propagation (:107), taken now, committed after the step
       double aF = (ln < (RED ? n + m : NS)) ? fabs(F) : 0.0;
       if (RED && rh) aF = max_nan(aF, fabs(Fc));
@@ -950,7 +1001,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         rhs = dot_strided<8, false>(ta + (ln < n ? ln : 0) * lda, 1, sT, m, rhs);
         sB[ln] = rhs;
       }
-      MCPX_STAMP(0);
+      MCPX_STAMP(1);
 
       // ---- dense LU with partial pivoting (:81-83) -----------------------
       double dz = 0.0;
@@ -962,6 +1013,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         if (spd_try) {  // S formed transposed on the matrix cores, Gauss-Jordan in that layout
           d4 acc4[NT][NT];
           qp_schur_form_2d<NT>(th, ta, lda, sD, ln, n, m, tol, acc4);
+          MCPX_STAMP(2);
           double acc[NT][NT][4];
 #pragma unroll
           for (int I = 0; I < NT; ++I)
@@ -970,14 +1022,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
 #pragma unroll
               for (int r = 0; r < 4; ++r) acc[I][J][r] = acc4[I][J][r];
           __syncthreads();  // rr (sB) of every row
-          double rh2[NT], x2[NT];
+          double rh2[NT];
 #pragma unroll
           for (int J = 0; J < NT; ++J) rh2[J] = (16 * J + (ln & 15) < n) ? sB[16 * J + (ln & 15)] : 0.0;
-          ok = gj2d_spd<NT, (NC == 0)>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, x2);  // opaque: with a constant
-          // dimension the scheduler merges the 32 steps (+5 % VALU in the fast pass)
-#pragma unroll
-          for (int J = 0; J < NT; ++J)
-            if ((ln >> 4) == J) dz = x2[J];  // lane 16J + lc owns row 16J + lc
+          // lane 16J + lc owns row 16J + lc.  Opaque dimension: with a constant one the
+          // scheduler merges the 32 steps (+5 % VALU in the fast pass)
+          ok = gj2d_spd<NT, (NC == 0)>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, dz);
         }
         if constexpr (PASS == 1) {
           if (!ok) {  // S not numerically SPD at this step: second pass
@@ -997,7 +1047,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       } else {
         ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);
       }
-      MCPX_STAMP(1);
+      MCPX_STAMP(3);
       if (!ok) {
         status = 1;
         break;
@@ -1014,7 +1064,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       }
       double ds = 0.0;
       if (RED && rh) ds = SCH ? fma(-s, dz, -Fc) * rw : fma(-s, dz, -Fc) / w;  // δs_k = (−F_Ck − s_k δy_k) / w_k
-      MCPX_STAMP(2);
+      MCPX_STAMP(4);
 
       // ---- fraction-to-the-boundary line search (:93-100, :127-138) -----
       const bool ry = rh;
@@ -1063,7 +1113,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         if (ry) z = z + ay * dz;
       }
       kkt = kkt_step;  // :107
-      MCPX_STAMP(3);
+      MCPX_STAMP(5);
       ++inner;         // :108
       ++newton;
     }
@@ -1096,7 +1146,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   }
 #if MCPX_STAMPS
   if (lane == 0 && args.stamps)
-    for (int i = 0; i < 4; ++i) args.stamps[inst * 4 + i] = st_acc[i];
+    for (int i = 0; i < MCPX_NSTAMP; ++i) args.stamps[inst * MCPX_NSTAMP + i] = st_acc[i];
 #endif
   if (lane == 0) {
     args.kkt_error[inst] = kkt;

@@ -112,6 +112,8 @@ def wait_state_hazards(insts, want: str):
             # lane select written by a VALU: 4 wait states (VGPR sources: none)
             checked += 1
             sel, states, j = sregs(ops[2]), 0, i - 1
+            if not sel:  # inline-constant lane select: nothing to wait for
+                continue
             while j >= 0 and states < 4:
                 kk, tt, _, ll = insts[j]
                 if kk != k or ll:

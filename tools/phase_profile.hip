@@ -44,7 +44,7 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&x, (size_t)B * n * 8); (void)hipMalloc(&y, (size_t)B * m * 8); (void)hipMalloc(&s, (size_t)B * m * 8);
   (void)hipMalloc(&kkt, B * 8); (void)hipMalloc(&eps, B * 8);
   (void)hipMalloc(&outer, B * 4); (void)hipMalloc(&status, B * 4); (void)hipMalloc(&newton, B * 4);
-  (void)hipMalloc(&stamps, (size_t)B * 4 * 8);
+  (void)hipMalloc(&stamps, (size_t)B * MCPX_NSTAMP * 8);
   mcpx::KernelArgs a;
   // reuse the ABI's parameter preparation through a normal call first (fills nothing here)
   std::memset((void*)&a, 0, sizeof a);
@@ -69,15 +69,15 @@ int main(int argc, char** argv) {
     if (e != hipSuccess) { printf("launch failed / unsupported mode: %s\n", hipGetErrorString(e)); return 1; }
     (void)hipDeviceSynchronize();
   }
-  std::vector<uint64_t> st((size_t)B * 4);
+  std::vector<uint64_t> st((size_t)B * MCPX_NSTAMP);
   std::vector<int> nw(B);
   (void)hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost);
   (void)hipMemcpy(nw.data(), newton, B * 4, hipMemcpyDeviceToHost);
-  double tot[4] = {0, 0, 0, 0}, nsteps = 0;
-  for (int b = 0; b < B; ++b) { for (int i = 0; i < 4; ++i) tot[i] += st[(size_t)b * 4 + i]; nsteps += nw[b]; }
-  const double all = tot[0] + tot[1] + tot[2] + tot[3];
-  const char* nm[] = {"assemble+kkt", "LU+fwd", "backsub", "linesearch+update"};
+  double tot[MCPX_NSTAMP] = {}, nsteps = 0, all = 0;
+  for (int b = 0; b < B; ++b) { for (int i = 0; i < MCPX_NSTAMP; ++i) tot[i] += st[(size_t)b * MCPX_NSTAMP + i]; nsteps += nw[b]; }
+  for (int i = 0; i < MCPX_NSTAMP; ++i) all += tot[i];
+  const char* nm[] = {"residuals", "kkt-norm+rr", "schur-form", "LU/GJ", "backsub", "linesearch+update"};
   printf("[%s] n=%d m=%d B=%d  mean newton %.2f  wave-cycles per Newton step %.0f\n", mode, n, m, B, nsteps / B, all / nsteps);
-  for (int i = 0; i < 4; ++i) printf("  %-18s %5.1f%%  %8.0f cyc/step\n", nm[i], 100 * tot[i] / all, tot[i] / nsteps);
+  for (int i = 0; i < MCPX_NSTAMP; ++i) printf("  %-18s %5.1f%%  %8.0f cyc/step\n", nm[i], 100 * tot[i] / all, tot[i] / nsteps);
   return 0;
 }
