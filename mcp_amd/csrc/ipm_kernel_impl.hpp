@@ -56,10 +56,6 @@
 #ifndef MCPX_FAST_WAVES
 #define MCPX_FAST_WAVES 5
 #endif
-// … and in the fast pass with the fused pullback (its register row is n + m wide).
-#ifndef MCPX_FUSED_WAVES
-#define MCPX_FUSED_WAVES 4
-#endif
 
 // Diagnostic phase stamps (tools/phase_profile.hip builds with MCPX_STAMPS=1;
 // the product build compiles them away).
@@ -821,9 +817,10 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
 
 // The rrule pullback fused into the solve kernel's epilogue (defined in
 // sens_kernel_impl.hpp; only the FUSE instantiations of ipm_inst_fused.hip use it).
-template <int NV, int FAMILY>
+template <int NV, int FAMILY, int NT, bool LU>
 __device__ __forceinline__ void fused_vjp(const KernelArgs& A, int64_t inst, int ln, int n, int m, double z, double s,
-                          const double* th);
+                                          const double* th, const double* ta, int lda, bool msym,
+                                          double* const (&lds)[5]);
 
 }  // namespace
 
@@ -870,7 +867,7 @@ __device__ __forceinline__ void schur_rows_from_2d(const d4 (&acc)[NT][NT], int 
 // FUSE > 0 (ipm_inst_fused.hip): the instance's rrule pullback runs in the epilogue
 // (fused_vjp, register width FUSE ≥ n + m) once its solve is final — mcpx_solve_vjp_batch_device.
 template <int NMAX, int FAMILY, int NC, int MC, int SOLVER, int PASS, int FUSE = 0>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? (FUSE > 0 ? MCPX_FUSED_WAVES : MCPX_FAST_WAVES) : 1, 8))) void ipm_solve_kernel(const KernelArgs args) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? MCPX_FAST_WAVES : 1, 8))) void ipm_solve_kernel(const KernelArgs args) {
   constexpr bool RED = SOLVER != MCPX_LINSOLVE_DENSE;  // lanes [0,n) x, [n,n+m) (y, s)
   constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR;
   static_assert(SCH || PASS == 0, "two-pass launch is for the SCHUR solver only");
@@ -880,6 +877,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   __shared__ double zs[64];
   __shared__ double sD[SCH ? 64 : 1], sT[SCH ? 64 : 1];  // SCHUR: D_k⁻¹, ty_k
   __shared__ double sB[SCH ? 64 : 1];  // rr, restored for the LU fallback
+  __shared__ double sF[FUSE > 0 ? 64 : 1];  // the fused pullback's fifth LDS array
   // SCHUR with compile-time (n, m): A (row i of Aᵀ at sA[i·LDA], odd stride: the
   // lanes' row reads fall in different banks), b and ϕ copied into LDS once per
   // instance; they are read five times per Newton step (residual rows of G and of H,
@@ -1157,7 +1155,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   }
   if constexpr (FUSE > 0) {
     static_assert(RED && FAMILY == MCPX_FAMILY_QP, "the fused pullback follows the QP REDUCED / SCHUR lane layout");
-    fused_vjp<FUSE, FAMILY>(args, inst, lane, n, m, z, s, th0);
+    // the pullback's Schur path reuses the solve's A block (LDS copy) and its M-symmetry test
+    // (opaque sizes: with constant ones the pullback's loops unroll into spills)
+    double* const lds[5] = {zs, sD, sT, sB, sF};
+    fused_vjp<FUSE, FAMILY, (NMAX + 15) / 16, PASS != 1>(args, inst, lane, opaque(n), opaque(m), z, s, th0,
+                                                         LDSA ? (const double*)sA : th0 + n * n, LDSA ? LDA : m,
+                                                         spd_try, lds);
   }
 }
 

@@ -301,18 +301,91 @@ __device__ __forceinline__ void vjp_reduced_row(const double* __restrict__ th, c
     for (int k = 0; k < m; ++k) rhs = fma(ph[k * sh], gsv[k], rhs);
 }
 
+// M exactly symmetric (the SCHUR solver's spd_try test; uniform).
+__device__ __forceinline__ bool m_symmetric(const double* __restrict__ th, int ln, int n) {
+  bool asym = false;
+  const int r = min(ln, max(n - 1, 0));
+  for (int j = 0; j < n; ++j) asym |= ln < n && !(th[j * n + r] == th[r * n + j]);
+  return ballot(asym) == 0ull;
+}
+
+// QP pullback by the Schur complement (oracle vjp_qp_schur): with d = y / s,
+//   (M + Aᵀ diag(d) A) λx = gx + Aᵀ (gs − d ⊙ gy),   λc = (gy + A λx) / s,
+// S' formed on the matrix cores exactly as the SCHUR solver forms S (tol = 0, D⁻¹ = d)
+// and solved by the 2-D Gauss-Jordan.  Needs M symmetric (msym), s > 0, y ≥ 0 and d
+// finite; false (→ the LU of the reduced system) otherwise or on a pivot ≤ 0.  On true,
+// l = this lane's entry of u = [λx; λc].  ta / lda: the A block (A_kj = ta[j·lda + k]);
+// LDS scratch of 64 doubles each: sd (d_k), tk (gs_k − d_k·gy_k, then λx_j), gxl (gx_j;
+// free again on return).
+template <int NT>
+__device__ __forceinline__ bool vjp_qp_schur(const double* __restrict__ th, const double* ta, int lda,
+                                             const double* zs, const double* gsv, double g, int ln, int n, int m,
+                                             bool msym, double* sd, double* tk, double* gxl, double& l) {
+  const bool rh = ln >= n && ln < n + m;
+  const int k = ln - n;
+  const double yk = rh ? zs[ln] : 1.0, sk = rh ? zs[ln + m] : 1.0;
+  const double d = yk / sk;
+  const bool okk = sk > 0.0 && yk >= 0.0 && __builtin_isfinite(d);
+  if (!msym || n < 1 || n > 16 * NT || ballot(rh && !okk) != 0ull) return false;
+  __syncthreads();  // scr may still be read by the caller's previous use
+  if (rh) {
+    sd[k] = d;
+    tk[k] = fma(-d, g, gsv ? gsv[k] : 0.0);
+  }
+  if (ln < n) gxl[ln] = g;
+  __syncthreads();
+  const int lc = ln & 15;
+  double rh2[NT];
+#pragma unroll
+  for (int J = 0; J < NT; ++J) {
+    const int j = 16 * J + lc;
+    rh2[J] = j < n ? dot_strided<8, false>(ta + j * lda, 1, tk, m, gxl[j]) : 0.0;
+  }
+  d4 acc4[NT][NT];
+  qp_schur_form_2d<NT>(th, ta, lda, sd, ln, n, m, 0.0, acc4);
+  double acc[NT][NT][4];
+#pragma unroll
+  for (int I = 0; I < NT; ++I)
+#pragma unroll
+    for (int J = 0; J < NT; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[I][J][r] = acc4[I][J][r];
+  double xo = 0.0;
+  if (!gj2d_spd<NT, true>(acc, rh2, n, ln, xo)) return false;
+  __syncthreads();  // every read of tk done
+  if (ln < n) tk[ln] = xo;
+  __syncthreads();
+  l = ln < n ? xo : 0.0;
+  if (rh) l = dot_strided<8, false>(ta + k, lda, tk, n, g) / sk;
+  return true;
+}
+
 // The pullback of one instance (the rrule of src/AutoDiff.jl:42-82), one wave: zs = z =
 // [x; y; s] in LDS, `lam` LDS scratch (≥ n+m), g = this lane's cotangent entry of the x / y
 // rows, gsv = the s block's cotangent (any address space) or NULL = zero.  Writes ∂θ
-// (family layout, stride p) to `o` and 0 / 1 (∇F_z singular) to *st.
-template <int NMAX, int FAMILY>
-__device__ __forceinline__ void vjp_instance(const double* __restrict__ th, const double* zs, double* lam,
+// (family layout, stride p) to `o` and 0 / 1 (∇F_z singular) to *st.  QP family with
+// NT > 0: the Schur-complement path first (vjp_qp_schur; ta / lda, msym, sd / tk as
+// there, `lam` its gxl).
+// LU = false (the fused fast pass): no LU fallback — returns false, writing nothing,
+// when the Schur path does not apply.
+template <int NMAX, int FAMILY, int NT = 0, bool LU = true>
+__device__ __forceinline__ bool vjp_instance(const double* __restrict__ th, const double* zs, double* lam,
                                              const double* gsv, double g, int ln, int n, int m, double* __restrict__ o,
-                                             int32_t* st) {
-  double a[NMAX];
-  vjp_reduced_row<NMAX, FAMILY>(th, zs, gsv, ln, n, m, a, g);
+                                             int32_t* st, const double* ta = nullptr, int lda = 0, bool msym = false,
+                                             double* sd = nullptr, double* tk = nullptr) {
   double l = 0.0;
-  const bool ok = lu_solve_rows<NMAX>(a, g, n + m, ln, l);
+  bool ok = false;
+  if constexpr (FAMILY == MCPX_FAMILY_QP && NT > 0)
+    ok = vjp_qp_schur<NT>(th, ta, lda, zs, gsv, g, ln, n, m, msym, sd, tk, lam, l);
+  if constexpr (LU) {
+    if (!ok) {
+      double a[NMAX];
+      vjp_reduced_row<NMAX, FAMILY>(th, zs, gsv, ln, n, m, a, g);
+      ok = lu_solve_rows<NMAX>(a, g, n + m, ln, l);
+    }
+  } else {
+    if (!ok) return false;
+  }
   // [λx; λc] → [λx; λh], λh_q = y_q·λc_q − gs_q
   double lv = l;
   if (ln >= n && ln < n + m) {
@@ -340,13 +413,17 @@ __device__ __forceinline__ void vjp_instance(const double* __restrict__ th, cons
     write_block(o + nn + 2 * nm + mm, n, 1, ln, [&](int i, int) { return -lx[i]; });       // ∂g_i
     write_block(o + nn + 2 * nm + mm + n, m, 1, ln, [&](int k, int) { return -ly[k]; });   // ∂h_k
   }
+  return true;
 }
 
 template <int NMAX, int FAMILY>
 __global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
+  constexpr bool QP = FAMILY == MCPX_FAMILY_QP;
+  constexpr int NT = QP ? (NMAX + 15) / 16 : 0;  // Schur path: n < NMAX
   __shared__ double zs[64];
   __shared__ double lam[64];
   __shared__ double gsl[64];
+  __shared__ double scr[QP ? 128 : 1];
   const int ln = threadIdx.x;
   const int64_t inst = blockIdx.x;
   const int n = A.n, m = A.m;
@@ -363,18 +440,24 @@ __global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
     __syncthreads();
     gsv = gsl;
   }
-  vjp_instance<NMAX, FAMILY>(th, zs, lam, gsv, g, ln, n, m, A.out + inst * A.p, A.status ? A.status + inst : nullptr);
+  const bool msym = QP && m_symmetric(th, ln, n);
+  vjp_instance<NMAX, FAMILY, NT>(th, zs, lam, gsv, g, ln, n, m, A.out + inst * A.p, A.status ? A.status + inst : nullptr,
+                                 th + (int64_t)n * n, m, msym, scr, scr + 64);
 }
 
 // The pullback fused into the solve kernel's epilogue (ipm_solve_kernel<…, FUSE = NV>):
 // the solve's lane layout (lanes [0, n) x, [n, n+m) y with s in `s`) into LDS, the
 // cotangent a ⊙ z + b of KernelArgs, vjp_instance with register width NV ≥ n + m.
-template <int NV, int FAMILY>
+// LU = false (fast pass): an instance the Schur path cannot take is deferred to the
+// second pass, which solves it again (same bits) and pulls back with the LU fallback.
+// lds: five 64-double LDS arrays of the solve kernel, dead once its outputs are written.
+template <int NV, int FAMILY, int NT, bool LU>
 __device__ __forceinline__ void fused_vjp(const KernelArgs& A, int64_t inst, int ln, int n, int m, double z, double s,
-                          const double* th) {
-  __shared__ double zs[64];
-  __shared__ double lam[64];
-  __shared__ double gsl[64];
+                                          const double* th, const double* ta, int lda, bool msym,
+                                          double* const (&lds)[5]) {
+  double* const zs = lds[0];
+  double* const lam = lds[1];
+  double* const gsl = lds[2];
   __syncthreads();
   if (ln < n + m) zs[ln] = z;
   if (ln >= n && ln < n + m) zs[ln + m] = s;
@@ -389,8 +472,10 @@ __device__ __forceinline__ void fused_vjp(const KernelArgs& A, int64_t inst, int
     gsv = gsl;
   }
   const int64_t p = (int64_t)n * n + (int64_t)m * n + m + n;  // QP θ dimension (mcpx_theta_dim)
-  vjp_instance<NV, FAMILY>(th, zs, lam, gsv, g, ln, n, m, A.vjp_dtheta + inst * p,
-                           A.vjp_status ? A.vjp_status + inst : nullptr);
+  const bool done = vjp_instance<NV, FAMILY, NT, LU>(th, zs, lam, gsv, g, ln, n, m, A.vjp_dtheta + inst * p,
+                                                     A.vjp_status ? A.vjp_status + inst : nullptr, ta, lda, msym,
+                                                     lds[3], lds[4]);
+  if (!done && ln == 0) A.status[inst] = STATUS_DEFERRED;
 }
 
 template <int NMAX, int FAMILY>

@@ -739,6 +739,57 @@ typedef struct sens_job {
   int err;
 } sens_job;
 
+/* QP family pullback by the Schur complement, for the one-wave sizes (n + 2m <=
+ * MCPX_MAX_KKT_DIM) with M exactly symmetric, every s_k > 0, y_k >= 0 and y_k / s_k
+ * finite.  The reduced system of sens_one (u = [λx; λc]) is, for the QP family,
+ *     M λx + Aᵀ diag(y) λc = gx + Aᵀ gs,      −A λx + diag(s) λc = gy;
+ * λc = (gy + A λx) / s leaves the n×n SPD system
+ *     (M + Aᵀ diag(d) A) λx = gx + Aᵀ (gs − d ⊙ gy),   d = y / s,
+ * whose matrix is formed exactly as the SCHUR solver forms S (tol = 0, D⁻¹ = d, the
+ * MFMA's K padding) and solved by gj_spd_solve.  Absent cotangent blocks are zeros here.
+ * On return 0, w->dz = [λx; λc]; 1: a condition or a pivot failed (→ the LU path). */
+static int vjp_qp_schur(int n, int m, const double* th, const double* z, const double* gx, const double* gy,
+                        const double* gs, sens_ws* w) {
+  if (n < 1 || n + 2 * m > MCPX_MAX_KKT_DIM) return 1;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j)
+      if (!(th[(size_t)j * n + i] == th[(size_t)i * n + j])) return 1;
+  const double* y = z + n;
+  const double* s = z + n + m;
+  const double* A = th + (size_t)n * n; /* A_kj = A[j·m + k] */
+  double* d = w->row;
+  double* t = w->b + n;                 /* gs − d ⊙ gy */
+  for (int k = 0; k < m; ++k) {
+    if (!(s[k] > 0.0) || !(y[k] >= 0.0)) return 1;
+    d[k] = y[k] / s[k];
+    if (!isfinite(d[k])) return 1;
+    t[k] = fma(-d[k], gy ? gy[k] : 0.0, gs ? gs[k] : 0.0);
+  }
+  double* S = w->J;
+  const int m4 = (m + 3) / 4 * 4;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double acc = th[(size_t)j * n + i]; /* M_ij */
+      if (i == j) acc = acc + 0.0;        /* the solver's + tol, tol = 0 */
+      for (int k = 0; k < m4; ++k)
+        acc = k < m ? fma(A[(size_t)i * m + k], A[(size_t)j * m + k] * d[k], acc) : fma(0.0, 0.0, acc);
+      S[(size_t)i * n + j] = acc;
+    }
+  double* r = w->b;
+  for (int j = 0; j < n; ++j) {
+    double acc = gx ? gx[j] : 0.0;
+    for (int k = 0; k < m; ++k) acc = fma(A[(size_t)j * m + k], t[k], acc);
+    r[j] = acc;
+  }
+  if (gj_spd_solve(n, S, r, w->dz)) return 1;
+  for (int k = 0; k < m; ++k) {
+    double acc = gy ? gy[k] : 0.0;
+    for (int j = 0; j < n; ++j) acc = fma(A[(size_t)j * m + k], w->dz[j], acc);
+    w->dz[n + k] = acc / s[k];
+  }
+  return 0;
+}
+
 static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
   const mcpx_desc* d = j->d;
   const int n = d->n, m = d->m, N = n + 2 * m;
@@ -772,11 +823,14 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
                      + Σ_k ∇F_z[n+k][n+q] gs_k
        (gs = NULL: the Σ gs chains are skipped), factored by lu_solve like the solver's
        REDUCED Newton system.  The GPU's vjp_kernel forms the same rows. */
-    jacobian_z(d->family, n, m, fth, w->z, w->J);
-    const int Nr = n + m;
     const double* yv = w->z + n;
     const double* sv = w->z + n + m;
-    for (int r = 0; r < Nr; ++r) {
+    const int Nr = n + m;
+    int schur = !j->nl && d->family == MCPX_FAMILY_QP &&
+                vjp_qp_schur(n, m, th, w->z, j->gx ? j->gx + b * n : NULL, j->gy ? j->gy + b * m : NULL,
+                             j->gs ? j->gs + b * m : NULL, w) == 0;
+    if (!schur) jacobian_z(d->family, n, m, fth, w->z, w->J);
+    for (int r = 0; r < Nr && !schur; ++r) {
       double* row = w->JT + (size_t)r * Nr;
       /* QP family, y-rows: ∂H/∂y ≡ 0 is a structural zero block — never multiplied, neither
          into the row (0 instead of 0·y_k) nor into the rhs (no fma(0, gs_k, ·)); the kernel
@@ -794,7 +848,7 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
         for (int k = 0; k < m; ++k) acc = fma(w->J[(size_t)(n + k) * N + r], j->gs[b * m + k], acc);
       w->b[r] = acc;
     }
-    failed = lu_solve(Nr, w->JT, w->b, w->dz, w->rem, w->step, w->prow);
+    failed = schur ? 0 : lu_solve(Nr, w->JT, w->b, w->dz, w->rem, w->step, w->prow);
     if (failed) {
       for (int i = 0; i < N; ++i) w->dz[i] = nanv;
     } else {  /* [λx; λc] → [λx; λh]: λh_k = y_k·λc_k − gs_k */
