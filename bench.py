@@ -261,7 +261,7 @@ def launch_ranks(nranks: int, script: str, argv, have_devices: int | None = None
 
 
 def evidence(name: str, cfg: dict) -> dict:
-    """The committed rocprofv3 summaries of this configuration (profiles/r02/
+    """The committed rocprofv3 summaries of this configuration (profiles/r03/
     trace_<name>.json, pmc_<name>.json; tools/prof_summary.py), if they were taken on
     exactly this configuration and this build of libmcpx.so; else {}."""
     from mcp_amd.build import built_hash
@@ -594,7 +594,7 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     G = pl["global_batch"]
     ls = a.linear_solver
     NS = solve_dim(n, m, ls)
-    cfg = {"mode": "c5" if a.sens else "c3", "n": n, "m": m, "batch_per_gpu": B, "linear_solver": ls,
+    cfg = {"mode": ("c5" if fused else "c5u") if a.sens else "c3", "n": n, "m": m, "batch_per_gpu": B, "linear_solver": ls,
            "sparsity": a.sparsity}
     key = f"{cfg['mode']}_n{n}_m{m}_b{B}_{ls}"
     ev = evidence(key, cfg)

@@ -1,14 +1,14 @@
 """A/B of generated-module kernel variants on the lane-change game (BASELINE C4).
 
-    python tools/ab_module.py build NAME CSRC_DIR [T]   # CPU: module text of T (default 2) + CSRC_DIR headers
-    python tools/ab_module.py run NAME... [--T T] [--B B]  # GPU: time each, compare with the oracle
+    python tests/ab/ab_module.py build NAME CSRC_DIR [T]   # CPU: module text of T (default 2) + CSRC_DIR headers
+    python tests/ab/ab_module.py run NAME... [--T T] [--B B]  # GPU: time each, compare with the oracle
 
 Variants are throwaway code objects under tools/abx/ (not kept in the tree); the
 generated text is the product's (mcp_amd/codegen.py), only the kernel headers differ."""
 import os, subprocess, sys, time
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "abx")
 

@@ -24,8 +24,7 @@ g = LaneChangeGame(2)
 mcp = g.mcp
 n, m = mcp.unconstrained_dimension, mcp.constrained_dimension
 th_host = np.ascontiguousarray(mcp.theta_map(chunked_slice(lambda r, k: g.generate_random_parameter(r, k), 1, 0, 1024)))
-mods = {"x2_shipped": mcp.module(), "x5_fixed": Module(os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                                    "su5_fixed.hsaco"))}
+mods = {"x2_shipped": mcp.module(), "x5_fixed": Module(os.path.join(ROOT, "tools", "ab_c4", "su5_fixed.hsaco"))}
 FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters")
 for B in (1, 1024):
     ref = coracle.solve_batch_nl(mcp.nl, th_host[:B], tol=1e-6, linear_solver="schur", nthreads=16)

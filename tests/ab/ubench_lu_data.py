@@ -1,10 +1,10 @@
 """Dumps Schur complements S (and rhs) of the lane-change game at T = 2 for tools/ubench_lu.hip:
 S = (P + tol·I) − Q D⁻¹ R at the iterate after a few outer iterations (oracle), rows
 canonicalised as the kernel does; and the oracle LU's solution for checking.
-    python tools/ubench_lu.py B   → tools/abx/lu_S.bin (B×40×41 doubles, row-major [S | rhs])"""
+    python tests/ab/ubench_lu_data.py B   → tools/ubench_data/lu_S.bin (B×40×41 doubles, row-major [S | rhs])"""
 import os, sys
 import numpy as np
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from mcp_amd.lane_change import LaneChangeGame
 from mcp_amd.qp_benchmark import chunked_slice
@@ -25,9 +25,8 @@ for b in range(B):
     S = P + tol * np.eye(n) - Q @ np.diag(1 / D) @ R
     out[b, :, :n] = S + 0.0
     out[b, :, n] = rng.standard_normal(n)
-os.makedirs(os.path.join(ROOT, "tools", "abx"), exist_ok=True)
-out.tofile(os.path.join(ROOT, "tools", "abx", "lu_S.bin"))
-pat = np.array(nl.schur_pattern(), dtype=np.uint64)
-pat.tofile(os.path.join(ROOT, "tools", "abx", "lu_pat.bin"))
-assert all(((out[b, i] [:n] != 0) <= ((int(pat[i]) >> np.arange(n)) & 1).astype(bool)).all() for b in range(B) for i in range(n))
+os.makedirs(os.path.join(ROOT, "tools", "ubench_data"), exist_ok=True)
+out.tofile(os.path.join(ROOT, "tools", "ubench_data", "lu_S.bin"))
+pat = np.full(n, (1 << 64) - 1, dtype=np.uint64)  # dense pattern (the sparse variant 6 reads it)
+pat.tofile(os.path.join(ROOT, "tools", "ubench_data", "lu_pat.bin"))
 print("wrote", out.shape)

@@ -133,3 +133,31 @@ def test_gpu_solve_vjp_warm_start_and_failures(gpu):
     for f in QP_FIELDS:
         assert _same(out[f].cpu().numpy(), ref[f].cpu().numpy()), f
     assert _same(dth.cpu().numpy(), rdth.cpu().numpy()) and _same(st.cpu().numpy(), rst.cpu().numpy())
+
+
+@pytest.mark.gpu
+def test_gpu_solve_vjp_asymmetric_m_takes_the_lu_pass(gpu, oracle_lib):
+    """M not exactly symmetric: the solve and the pullback both leave the Gauss-Jordan /
+    Schur paths (fast pass defers, second pass uses the LU fallbacks); same bits as the
+    composed calls and the oracle."""
+    import torch
+
+    from mcp_amd.batch import alloc_device_outputs, solve_batch_device, solve_vjp_batch_device, vjp_batch_device
+
+    rng = np.random.default_rng(5)
+    n, m, B = 32, 16, 256
+    th_h = generate_random_parameter(rng, n, m, 0.0, batch=B)
+    th_h[::2, 1] += 1e-3  # M[1, 0] != M[0, 1] in every other instance
+    dev = torch.device("cuda", 0)
+    th = torch.from_numpy(th_h).to(dev)
+    kw = dict(tol=1e-6, linear_solver="schur")
+    out, dth, st = solve_vjp_batch_device(0, n, m, th, ct=(2.0, 2.0, 0.0), **kw)
+    ref = solve_batch_device(0, n, m, th, alloc_device_outputs(B, n, m, dev), **kw)
+    rdth, rst = vjp_batch_device(0, n, m, th, ref["x"], ref["y"], ref["s"], 2.0 * ref["x"], 2.0 * ref["y"])
+    torch.cuda.synchronize()
+    for f in QP_FIELDS:
+        assert _same(out[f].cpu().numpy(), ref[f].cpu().numpy()), f
+    assert _same(dth.cpu().numpy(), rdth.cpu().numpy()) and _same(st.cpu().numpy(), rst.cpu().numpy())
+    x, y, s = (ref[f].cpu().numpy() for f in ("x", "y", "s"))
+    odth, ost = oracle_lib.vjp_batch(0, n, m, th_h, x, y, s, 2.0 * x, 2.0 * y, None)
+    assert _same(dth.cpu().numpy(), odth) and _same(st.cpu().numpy(), ost)

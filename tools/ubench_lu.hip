@@ -1,8 +1,8 @@
-// LU microbenchmark on the lane-change Schur complements (tools/ubench_lu.py dumps them):
+// LU microbenchmark on the lane-change Schur complements (tests/ab/ubench_lu_data.py dumps them):
 // one 64-lane wave per instance (row per lane, NMAX = 40), cycles per factorisation +
 // solve (s_memtime) of LU variants, and their solutions (bitwise checked on the host).
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -mllvm -amdgpu-mfma-vgpr-form=1
-//        -I mcp_amd/csrc tools/ubench_lu.hip -o tools/abx/ubench_lu
+//        -I mcp_amd/csrc tools/ubench_lu.hip -o tools/ubench_data/ubench_lu
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -50,10 +50,10 @@ int main(int argc, char** argv) {
   const int B = 256, reps = argc > 1 ? atoi(argv[1]) : 20;
   std::vector<double> S((size_t)B * NM * (NM + 1));
   std::vector<uint64_t> pat(NM);
-  FILE* f = fopen("tools/abx/lu_S.bin", "rb");
+  FILE* f = fopen("tools/ubench_data/lu_S.bin", "rb");
   fread(S.data(), sizeof(double), S.size(), f);
   fclose(f);
-  f = fopen("tools/abx/lu_pat.bin", "rb");
+  f = fopen("tools/ubench_data/lu_pat.bin", "rb");
   fread(pat.data(), 8, NM, f);
   fclose(f);
   double *dS, *dX;
@@ -68,7 +68,7 @@ int main(int argc, char** argv) {
   hipMemset(dpk, 0, (size_t)B * 64 * 4);
   hipMemcpy(dS, S.data(), S.size() * 8, hipMemcpyHostToDevice);
   hipMemcpy(dP, pat.data(), NM * 8, hipMemcpyHostToDevice);
-  std::vector<double> X0((size_t)B * 64), X((size_t)B * 64);
+  std::vector<double> X0((size_t)B * 64), X1((size_t)B * 64), X((size_t)B * 64);
   std::vector<unsigned long long> C(B);
 #define RUN(V)                                                                                       \
   {                                                                                                  \
@@ -76,14 +76,17 @@ int main(int argc, char** argv) {
     hipDeviceSynchronize();                                                                          \
     hipMemcpy(X.data(), dX, X.size() * 8, hipMemcpyDeviceToHost);                                    \
     hipMemcpy(C.data(), dC, B * 8, hipMemcpyDeviceToHost);                                           \
+    if (V == 1) X1 = X;                                                                              \
     if (V == 4) X0 = X;                                                                              \
     double s = 0;                                                                                    \
     for (auto c : C) s += c;                                                                         \
     size_t diff = 0;                                                                                 \
     for (size_t q = 0; q < X.size(); ++q) diff += (X[q] != X0[q]) && !(X[q] != X[q] && X0[q] != X0[q]); \
-    printf("variant %d (%s): %8.0f cycles per LU+solve (mean of %d waves), entries differing from v4: %zu\n", \
-           V, variant_name(V), s / B, B, diff);                                                      \
+    size_t diff1 = 0;                                                                                \
+    for (size_t q = 0; q < X.size(); ++q) diff1 += (X[q] != X1[q]) && !(X[q] != X[q] && X1[q] != X1[q]); \
+    printf("variant %d (%s): %8.0f cycles per LU+solve (mean of %d waves), entries differing from v4: %zu, from v1: %zu\n", \
+           V, variant_name(V), s / B, B, diff, diff1);                                               \
   }
-  RUN(0) RUN(1) RUN(4) RUN(9) RUN(10)
+  RUN(0) RUN(1) RUN(4) RUN(9) RUN(11) RUN(12)
   return 0;
 }
