@@ -705,15 +705,24 @@ def main(argv=None):
     if a.gpus > 1 and a.gpus != world:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
-    if world > 1 and torch.cuda.device_count() < world:
+    # MCPX_BENCH_SHARED_GPU=1: rehearsal of the N-rank path on a one-GPU box — every rank on
+    # cuda:0, gloo instead of RCCL (the sharding, the solves, the gather and the max-over-ranks
+    # timing run as on N GPUs; the rate is not an N-GPU rate)
+    shared = os.environ.get("MCPX_BENCH_SHARED_GPU") == "1"
+    if world > 1 and not shared and torch.cuda.device_count() < world:
         print(f"bench.py: {world} ranks but only {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
         return 2
     distributed = world > 1 or (a.gather and "RANK" in os.environ)
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("NCCL_DEBUG", "WARN")  # keep RCCL's banner off stdout (one JSON line)
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            local = 0
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     pl = plan(a, world, rank)
     try:
         if a.lane_change:

@@ -177,7 +177,9 @@ int mcpx_device_count(void);
  * the outputs back.  Blocking.  Per device the shard is pipelined in chunks on
  * two streams (the upload of chunk c+1 overlaps the solve of chunk c); θ in a
  * range registered with mcpx_host_register is read by DMA straight from the
- * caller's pages, any other θ is staged by the HIP runtime. */
+ * caller's pages, any other θ is staged by the HIP runtime.  The environment
+ * variable MCPX_HOST_SHARDS = k (tests) splits the batch into k shards over the
+ * visible devices round-robin, one host thread each, as k devices would. */
 int mcpx_solve_batch(const mcpx_desc* desc, const double* theta,
                      const double* x0, const double* y0, const double* s0,
                      const mcpx_params* prm, int num_devices, mcpx_out* out);

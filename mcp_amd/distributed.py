@@ -100,6 +100,10 @@ class Gatherer:
         self.girec = torch.empty(self.world * packed.irec.numel(), dtype=packed.irec.dtype,
                                  device=packed.irec.device)
         self._into = dist.get_backend(group) != "gloo"  # gloo lacks all_gather_into_tensor
+        # gloo gathers host tensors only: device records are staged through host copies
+        self._stage = not self._into and packed.rec.is_cuda
+        if self._stage:
+            self._h = [torch.empty_like(t, device="cpu") for t in (packed.rec, packed.irec, self.grec, self.girec)]
 
     def __call__(self):
         import torch.distributed as dist
@@ -107,6 +111,14 @@ class Gatherer:
         if self._into:
             dist.all_gather_into_tensor(self.grec, self.p.rec, group=self.group)
             dist.all_gather_into_tensor(self.girec, self.p.irec, group=self.group)
+        elif self._stage:
+            rec, irec, grec, girec = self._h
+            rec.copy_(self.p.rec)
+            irec.copy_(self.p.irec)
+            dist.all_gather(list(grec.chunk(self.world)), rec, group=self.group)
+            dist.all_gather(list(girec.chunk(self.world)), irec, group=self.group)
+            self.grec.copy_(grec)
+            self.girec.copy_(girec)
         else:
             dist.all_gather(list(self.grec.chunk(self.world)), self.p.rec, group=self.group)
             dist.all_gather(list(self.girec.chunk(self.world)), self.p.irec, group=self.group)
