@@ -211,6 +211,8 @@ def parse(argv=None):
                          "mcpx_vjp_batch_device) instead of mcpx_solve_vjp_batch_device")
     ap.add_argument("--gather", action="store_true",
                     help="run the RCCL result collection even at world size 1 (rehearsal under torchrun)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "workgroup", "multiwave"],
+                    help="with --lane-change: the generated module's kernel (mcpx_params.kernel)")
     ap.add_argument("--lane-change", type=int, default=0, metavar="T",
                     help="BASELINE C4: each step solves lane-change games of horizon T (generated "
                          "nonlinear module; examples/lane_change.jl, benchmark/trajectory_game_benchmark.jl)")
@@ -428,7 +430,7 @@ def main_lane_change(a, world, rank, local, dist, pl):
         if evs:
             evs[0][0].record(stream)
         solve_batch_device(_abi.FAMILY_NONLINEAR, n, m, theta, out, tol=a.tol, linear_solver=ls, stream=stream,
-                           module=module)
+                           module=module, kernel=a.kernel)
         if evs:
             evs[0][1].record(stream)
 
@@ -444,10 +446,12 @@ def main_lane_change(a, world, rank, local, dist, pl):
     # the generated module's content hash (its kernel headers included) keys the evidence too:
     # the nonlinear kernels live in the module, not in libmcpx.so
     cfg = {"mode": "c4", "horizon": a.lane_change, "batch_per_gpu": B, "linear_solver": ls,
-           "module": mcp.nl.module_key()}
+           "module": mcp.nl.module_key(), "kernel": a.kernel}
     key = f"c4_lane_t{a.lane_change}_b{B}"
     ev = evidence(key, cfg)
-    kernel = "mcpx_nl_solve_" + ls + ("" if mcp.nl.solvers()[ls] else "_wg")
+    mw = ls == "schur" and a.kernel == "multiwave" and module.has_schur_mw
+    kernel = "mcpx_nl_solve_" + ls + ("_mw" if mw else ("" if mcp.nl.solvers()[ls] and a.kernel != "workgroup"
+                                                         else "_wg"))
     rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops_nl(mcp.nl, ls),
                   B * 8.0 * (mcp.nl.p + n + 2 * m + 2) + 12.0 * B, ev, kernel, roofline_bound(ev, kern_ms, "latency"),
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system per Newton step) "

@@ -84,10 +84,15 @@ extern "C" {
  *  MCPX_KERNEL_WAVE       only the one-wave kernels (MCPX_EUNSUPPORTED beyond);
  *  MCPX_KERNEL_WORKGROUP  the workgroup-per-instance kernels at any size they
  *                         support (REDUCED / DENSE, and SCHUR for generated
- *                         modules) — bit-identical results to the one-wave path. */
+ *                         modules) — bit-identical results to the one-wave path;
+ *  MCPX_KERNEL_MULTIWAVE  generated modules, SCHUR: one 4-wave workgroup per
+ *                         instance, S in LDS, the LU's columns split over the waves
+ *                         (module kernel-mask bit MCPX_MODULE_SCHUR_MW); same bits,
+ *                         opt-in (slower than one wave on the lane-change game). */
 #define MCPX_KERNEL_AUTO 0
 #define MCPX_KERNEL_WAVE 1
 #define MCPX_KERNEL_WORKGROUP 2
+#define MCPX_KERNEL_MULTIWAVE 3
 /* largest max_inner_iters (ϵ-schedule table length) */
 #define MCPX_MAX_INNER_ITERS 128
 /* largest number of line-search trials (α = decayᵉ, e = 0..E) */
@@ -295,6 +300,7 @@ typedef struct mcpx_module mcpx_module;
 /* Sensitivity kernels of a module (bits of the mcpx_module_dims kernel mask) */
 #define MCPX_MODULE_VJP 6
 #define MCPX_MODULE_JVP 7
+#define MCPX_MODULE_SCHUR_MW 8  /* the 4-wave SCHUR solve kernel (MCPX_KERNEL_MULTIWAVE) */
 /* Loads the code object at `path` on the current device (other devices load
  * it on first use).  No usable GPU: MCPX_ENODEV. */
 int mcpx_module_load(const char* path, mcpx_module** mod);

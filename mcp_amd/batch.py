@@ -53,6 +53,10 @@ class Module:
     def has_jvp(self) -> bool:
         return bool((self.solvers >> _abi.MODULE_JVP) & 1)
 
+    @property
+    def has_schur_mw(self) -> bool:
+        return bool((self.solvers >> _abi.MODULE_SCHUR_MW) & 1)
+
     def close(self) -> None:
         if self.handle:
             lib().mcpx_module_unload(self.handle)

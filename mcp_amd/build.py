@@ -94,6 +94,7 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     if out is None and not force and not _stale():
         return LIB
     t0 = time.time()
+    stamp = source_hash(extra_flags)  # of the sources as they are when the compiles start
     objs, procs = [], []
     jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 1)
     tmp_dir = tempfile.mkdtemp(prefix="mcpx_build_")
@@ -152,7 +153,7 @@ def build(force: bool = False, verbose: bool = False, extra_flags=(), out: str |
     os.replace(tmp, lib_path)
     if out is None:
         with open(STAMP, "w") as f:
-            f.write(source_hash(extra_flags) + "\n")
+            f.write(stamp + "\n")
     shutil.rmtree(tmp_dir, ignore_errors=True)
     if verbose:
         print(f"built {lib_path} in {time.time() - t0:.1f}s", flush=True)

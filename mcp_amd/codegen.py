@@ -73,7 +73,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 Z_VOLATILE_ABOVE = int(os.environ.get("MCPX_NL_Z_VOLATILE_ABOVE", "128"))
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
-GEN_VERSION = 5
+GEN_VERSION = 6
+EVAL_PARTS = 4  # mcpx_nl_eval_p0..p3: the generated eval split over the 4-wave SCHUR kernel
 _MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function",
                  "-mllvm", "-amdgpu-mfma-vgpr-form=1")
 _MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "ipm_wg.h",
@@ -298,6 +299,60 @@ class NLSystem:
             lines.append(f"  {out}[{idx}] = {pr(e)};")
         return lines
 
+    def _block_parts(self, entries, with_z: bool, parts: int, out: str = "blk") -> list:
+        """`entries` split into `parts` straight-line functions' bodies for the 4-wave
+        SCHUR kernel (one wave's lane 0 runs each): the same CSE as _block, so every
+        output is the same expression tree (same bits); contiguous runs of entries (they
+        share temporaries) of about equal operation count; a temporary a part needs is
+        recomputed in that part."""
+        sp = _sp()
+        names = {t: f"th[{k}]" for k, t in enumerate(self.ts)}
+        if with_z:
+            names.update({x: f"MCPX_NL_Z({j})" for j, x in enumerate(self.xs)})
+            names.update({y: f"MCPX_NL_Z({self.n + k})" for k, y in enumerate(self.ys)})
+        if not entries:
+            return [[] for _ in range(parts)]
+        reps, red = sp.cse([e for _, e in entries], symbols=sp.numbered_symbols("c"), order="canonical")
+        rep_of = {sym: e for sym, e in reps}
+        order = {sym: i for i, (sym, _) in enumerate(reps)}
+
+        def need(e, have):
+            got, stack = set(), [e]
+            while stack:
+                for f in stack.pop().free_symbols:
+                    if f in rep_of and f not in got and f not in have:
+                        got.add(f)
+                        stack.append(rep_of[f])
+            return sorted(got, key=order.get)
+
+        # cost of each entry in sequence (its new temporaries included), then equal-cost runs
+        have, cost = set(), []
+        for e in red:
+            new = need(e, have)
+            have.update(new)
+            cost.append(1 + sp.count_ops(e) + sum(sp.count_ops(rep_of[t]) for t in new))
+        total, acc, cut, bounds = sum(cost), 0, 1, [0]
+        for i, c in enumerate(cost):
+            acc += c
+            if cut < parts and acc >= total * cut / parts:
+                bounds.append(i + 1)
+                cut += 1
+        while len(bounds) < parts:
+            bounds.append(len(red))
+        bounds.append(len(red))
+        bodies = []
+        for w in range(parts):
+            pr = _Printer(dict(names))
+            emitted, lines = set(), []
+            for (idx, _), e in list(zip(entries, red))[bounds[w]:bounds[w + 1]]:
+                for sym in need(e, emitted):
+                    lines.append(f"  const double {sym} = {pr(rep_of[sym])};")
+                    pr.names[sym] = str(sym)
+                    emitted.add(sym)
+                lines.append(f"  {out}[{idx}] = {pr(e)};")
+            bodies.append(lines)
+        return bodies
+
     def structure(self):
         """Structural nonzeros of Q = ∂G/∂y by rows (K(i): the k with Q_ik written by the
         generated code, ascending) and of R = ∂H/∂x by rows (J(k), ascending), as CSR
@@ -327,6 +382,12 @@ class NLSystem:
         init = self._block(self.const_entries, with_z=False)
         ev = self._block(self.var_entries + self.residuals, with_z=True)
         evt = self._block(self.theta_entries, with_z=True, out="dth")
+        evp = self._block_parts(self.var_entries + self.residuals, True, EVAL_PARTS)
+        parts = []
+        for w, body in enumerate(evp):
+            parts += [f"MCPX_NL_FN void mcpx_nl_eval_p{w}(const double* MCPX_NL_RESTRICT th, "
+                      "const double* MCPX_NL_RESTRICT z, double* MCPX_NL_RESTRICT blk) {",
+                      "  (void)th;", "  (void)z;", "  (void)blk;", *body, "}"]
         (qp, qi), (rp, ri) = self.structure()
         (tcp, tci), (trp, tri) = self.theta_structure()
         arr = lambda name, v: f"MCPX_NL_TABLE int32_t {name}[{max(len(v), 1)}] = {{{', '.join(map(str, v)) or '0'}}};"
@@ -362,6 +423,9 @@ class NLSystem:
             "  (void)z;",
             *ev,
             "}",
+            f"/* the same outputs in {EVAL_PARTS} parts (one per wave of mcpx_nl_solve_schur_mw) */",
+            f"#define MCPX_NL_EVAL_PARTS {EVAL_PARTS}",
+            *parts,
             "MCPX_NL_FN void mcpx_nl_eval_theta(const double* MCPX_NL_RESTRICT th, const double* MCPX_NL_RESTRICT z,",
             "                                   double* MCPX_NL_RESTRICT dth) {",
             "  (void)th;",

@@ -339,13 +339,17 @@ __device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, in
 #ifndef MCPX_LU_NO_SPEC
 #define MCPX_LU_NO_SPEC 0
 #endif
-template <int NMAX>
+// RCP (the SCHUR step of generated nonlinear modules, oracle lu_solve_x rcp): multipliers
+// a_ik · (1 / piv) and back substitution x_k = b_p · (1 / u_kk), one correctly rounded
+// reciprocal (rcp_uniform) per pivot.
+template <int NMAX, bool RCP = false>
 __device__ __forceinline__ bool lu_solve_rows_core(double (&a)[NMAX], double rhs, int N, int ln, double& dz,
                                                    int& pk, bool spec, bool& miss) {
   uint64_t rem = (N >= 64) ? ~0ull : ((1ull << N) - 1ull);
   int my_step = 1 << 30;  // LU step at which this row became a pivot row
   bool singular = false;
   bool viol = false;  // spec: a remaining row beats the guessed pivot under the first-max rule
+  double rcpd = 1.0;  // RCP: lane k holds 1 / u_kk of step k
   miss = false;
 #pragma clang loop unroll(full)
   for (int k = 0; k < NMAX; ++k) {
@@ -391,7 +395,15 @@ __device__ __forceinline__ bool lu_solve_rows_core(double (&a)[NMAX], double rhs
     rem &= ~(1ull << p);
     if (ln == p) my_step = k;
     if (ln == k) pk = p;
-    eliminate_row<NMAX>(a, rhs, k, ak / piv, 1ull << p, (rem >> ln) & 1ull);
+    double l;
+    if constexpr (RCP) {
+      const double rp = rcp_uniform(piv);
+      if (ln == k) rcpd = rp;
+      l = ak * rp;
+    } else {
+      l = ak / piv;
+    }
+    eliminate_row<NMAX>(a, rhs, k, l, 1ull << p, (rem >> ln) & 1ull);
   }
   if (spec && ballot(viol)) miss = true;
   if (singular || miss) return false;
@@ -400,8 +412,9 @@ __device__ __forceinline__ bool lu_solve_rows_core(double (&a)[NMAX], double rhs
   for (int k = NMAX - 1; k >= 0; --k) {
     if (k < N) {
       const int p = __builtin_amdgcn_readlane(pk, k);
-      const double t = rhs / a[k];
-      const double xk = bcast(t, p);
+      double xk;
+      if constexpr (RCP) xk = bcast(rhs, p) * bcast(rcpd, k);
+      else xk = bcast(rhs / a[k], p);
       if (ln == k) dz = xk;
       if (my_step < k) rhs = fma(-a[k], xk, rhs);
     }

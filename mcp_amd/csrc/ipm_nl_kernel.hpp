@@ -36,6 +36,8 @@
 #error "ipm_nl_kernel.hpp closes a generated module: MCPX_NL_* and mcpx_nl_init/eval come first"
 #endif
 
+#include <utility>
+
 namespace mcpx {
 namespace nl {
 
@@ -53,7 +55,241 @@ constexpr int rows_of(int solver) {
   return solver == MCPX_LINSOLVE_DENSE ? N : (solver == MCPX_LINSOLVE_REDUCED ? n + m : n);
 }
 
-template <int SOLVER>
+// ---- 2-D Gauss elimination of the one-wave SCHUR kernel ------------------------------
+// LU of [S | rr] with the previous Newton step's pivot sequence (lane k of pk = row p_k)
+// as the guess, in the matrix-core layout of the QP Gauss-Jordan (csrc/ipm_kernel_impl.hpp,
+// gj2d_spd): lane (lr, lc) holds position q = lc + 16J (J < NJ) at columns lr + 4c (c < NCB),
+// position q being row p_q, so step k's pivot is position k and its row reaches every lane
+// through DPP row_newbcast operands of the fmas; the pivot column goes to every lane by
+// ds_bpermute.  Multipliers a_qk · (1 / piv) (oracle lu_solve_x, rcp).  Finished halves are
+// skipped; rows of the pivot half at or before the pivot take the update with multiplier +0
+// (their lanes are the DPP sources); columns ≤ k of a straddling 4-column block are updated
+// too and never read again.  Each step checks the first-max rule against the guess on the
+// 64-bit |a| keys (a NaN entry counts as a violation); a violation or a zero / NaN guessed
+// pivot returns false with Srow untouched, for the searched LU.  On success the U rows go to
+// Srow and the substitution x_k = b_k · (1 / u_kk) runs lane per row; dz = x of row `ln`.
+template <int NM>
+struct Lu2d {
+  static constexpr int NJ = (NM + 15) / 16, NCB = (NM + 3) / 4;
+};
+
+template <int NM, int K>
+__device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
+                                          const int (&pv)[Lu2d<NM>::NJ], int pkk, int ln, uint32_t& viol,
+                                          double& rpv, bool& sing) {
+  constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
+  constexpr int Jk = K >> 4, Rk = K & 15, Qk = K & 3, Ck = K >> 2;
+  __builtin_amdgcn_sched_barrier(0);  // one step at a time: no step's uniform values hoisted ahead
+  const int lc = ln & 15;
+  const double piv = bcast(acc[Jk][Ck], 16 * Qk + Rk);
+  if (!(fabs(piv) > 0.0)) {
+    sing = true;
+    return;
+  }
+  const double rp = rcp_uniform(piv);
+  if (ln == K) rpv = rp;
+  const int64_t kp = (int64_t)((uint64_t)__double_as_longlong(piv) & 0x7fffffffffffffffull);
+  double nlm[NJ];
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) {
+    if (J < Jk) continue;
+    const double v = bperm_f64_addr(acc[J][Ck], (16 * Qk + lc) << 2);  // a_qk of position q = lc + 16J
+    const int q = lc + 16 * J;
+    const bool remq = (q > K) & (q < NM);
+    const int64_t kq = (int64_t)((uint64_t)__double_as_longlong(v) & 0x7fffffffffffffffull);
+    const int64_t d = (kp - (int64_t)(pv[J] < pkk)) - kq;
+    viol |= (uint32_t)((uint64_t)d >> 63) & (uint32_t)remq;
+    nlm[J] = remq ? -(v * rp) : 0.0;
+  }
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) {
+    if (J <= Jk) continue;
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      if (4 * c + 3 <= K) continue;
+      fmac_row_bcast<Rk, false>(acc[J][c], acc[Jk][c], nlm[J]);
+    }
+    fmac_row_bcast<Rk, false>(rh[J], rh[Jk], nlm[J]);
+  }
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    if (4 * c + 3 <= K) continue;
+    fmac_row_bcast_self<Rk, false>(acc[Jk][c], nlm[Jk]);
+  }
+  fmac_row_bcast_self<Rk, false>(rh[Jk], nlm[Jk]);
+}
+
+template <int NM, int... K>
+__device__ __forceinline__ void lu2d_steps(std::integer_sequence<int, K...>,
+                                           double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
+                                           const int (&pv)[Lu2d<NM>::NJ], int pk, int ln, uint32_t& viol, double& rpv,
+                                           bool& sing) {
+  ((sing ? void() : lu2d_step<NM, K>(acc, rh, pv, __builtin_amdgcn_readlane(pk, K), ln, viol, rpv, sing)), ...);
+}
+
+template <int NM>
+__device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk, double& dz) {
+  constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
+  const int lr = ln >> 4, lc = ln & 15;
+  double acc[NJ][NCB], rh[NJ];
+  int pv[NJ];
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) {
+    const int q = lc + 16 * J;
+    const int p = __builtin_amdgcn_ds_bpermute(min(q, 63) << 2, pk);  // row p_q of position q
+    pv[J] = q < NM ? p : 1 << 20;
+    const double* row = Srow + (q < NM ? p : 0) * LDR;
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) acc[J][c] = (q < NM && lr + 4 * c < NM) ? row[lr + 4 * c] : 0.0;
+    rh[J] = q < NM ? row[NM] : 0.0;
+  }
+  uint32_t viol = 0;
+  double rpv = 0.0;
+  bool sing = false;
+  lu2d_steps<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, pv, pk, ln, viol, rpv, sing);
+  if (sing || ballot(viol != 0)) return false;
+  __syncthreads();  // every row read before U overwrites Srow
+  // U by position (row q of the elimination = the guess's row p_q) and the reduced rhs
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) {
+    const int q = lc + 16 * J;
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+      if (q < NM && lr + 4 * c < NM) Srow[q * LDR + lr + 4 * c] = acc[J][c];
+    if (q < NM && lr == 0) Srow[q * LDR + NM] = rh[J];
+  }
+  __syncthreads();
+  double u[NM];
+  const int qq = ln < NM ? ln : 0;
+#pragma unroll
+  for (int j = 0; j < NM; ++j) u[j] = Srow[qq * LDR + j];
+  double b = Srow[qq * LDR + NM];
+  // a non-finite U entry or rhs: the +0-multiplier updates of the pivot half may have turned
+  // an entry the searched LU keeps into NaN — let the searched LU decide
+  bool fin = __builtin_isfinite(b);
+#pragma unroll
+  for (int j = 0; j < NM; ++j) fin = fin & ((j < ln) | __builtin_isfinite(u[j]));
+  if (ballot(!fin & (ln < NM))) return false;
+  double x = 0.0;
+#pragma unroll
+  for (int k = NM - 1; k >= 0; --k) {
+    const double xk = bcast(b, k) * bcast(rpv, k);  // position k's x, i.e. x of column k
+    if (ln == k) x = xk;
+    if (ln < k) b = fma(-u[k], xk, b);
+  }
+  dz = x;  // x_k = δ of column k: lane k holds unknown k
+  return true;
+}
+
+// ---- multi-wave LU of the SCHUR kernel (mcpx_nl_solve_schur_mw) ---------------------
+// First-max partial pivoting over the remaining rows (lu_solve_rows_core's search: keys
+// hi32(|a|)+1, NaN never wins, ties to the lowest row).
+__device__ __forceinline__ int pivot_search(double ak, uint64_t rem, int ln) {
+  const double av = fabs(ak);
+  const bool valid = ((rem >> ln) & 1ull) && !(av != av);
+  const uint32_t khi = valid ? (uint32_t)__double2hiint(av) + 1u : 0u;
+  const uint32_t mhi = wave_max_u32(khi);
+  if (mhi == 0u) return lowest_lane(rem);  // every remaining entry is NaN
+  const uint64_t cand = ballot(khi == mhi);
+  if (__popcll(cand) == 1) return lowest_lane(cand);
+  const uint32_t klo = (khi == mhi) ? (uint32_t)__double2loint(av) : 0u;
+  const uint32_t mlo = wave_max_u32(klo);
+  return lowest_lane(ballot(khi == mhi && klo == mlo));
+}
+
+// Pivot k from its column (this lane's entry ak): the multipliers a_ik / piv and the
+// pivot row (−1: a zero pivot, the failed solve of src/solver.jl:84-88) into the LDS
+// buffers of parity k.
+__device__ __forceinline__ void publish_pivot(int k, double ak, uint64_t rem, int ln, double* Lb, int* Pb) {
+  const int p = pivot_search(ak, rem, ln);
+  const double piv = bcast(ak, p);
+  Lb[(k & 1) * 64 + ln] = ak * rcp_uniform(piv);  // oracle lu_solve_x, rcp
+  if (ln == 0) Pb[k & 1] = (piv == 0.0) ? -1 : p;
+}
+
+// LU with partial pivoting of [S | rhs] (row i at Srow[i·LDR], rhs in column NC) on W waves,
+// then the solve: the oracle's lu_solve operation for operation (bit-identical).  Wave w
+// owns columns [w·CW, (w+1)·CW) of every row (lane i = row i), the last wave also the
+// right-hand side.  Per pivot the owner of the pivot column searches it and publishes the
+// multipliers and the pivot row through LDS (double-buffered: one barrier per pivot); every
+// wave then updates its columns with the pivot row broadcast from lane p.  The owner of
+// column k+1 updates that column first and publishes pivot k+1 before its other columns, so
+// the pivot chain runs ahead of the bulk of the update.  The U rows go back to LDS and
+// wave 0 runs the back substitution.  dz: the solution entry of row `ln` on wave 0.
+template <int NC, int W, int NMAX>
+__device__ __forceinline__ bool lu_solve_mw(double* Srow, int LDR, double* Lb, int* Pb, int* pv, int wv, int ln,
+                                            double& dz) {
+  constexpr int CW = (NC + W - 1) / W;
+  static_assert(CW + 1 <= 16, "one broadcast group per wave and pivot");
+  double acol[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int j = wv * CW + c;
+    acol[c] = (c < CW && ln < NC && j < NC) ? Srow[ln * LDR + j] : 0.0;
+  }
+  const bool rhs_wave = wv == W - 1;
+  if (rhs_wave) acol[CW] = ln < NC ? Srow[ln * LDR + NC] : 0.0;
+  uint64_t rem = (NC >= 64) ? ~0ull : ((1ull << NC) - 1ull);
+  int my_step = 1 << 30;
+  if (wv == 0) publish_pivot(0, acol[0], rem, ln, Lb, Pb);
+#pragma clang loop unroll(full)
+  for (int k = 0; k < NC; ++k) {
+    __syncthreads();
+    const int p = __builtin_amdgcn_readfirstlane(Pb[k & 1]);
+    if (p < 0) return false;
+    const double l = Lb[(k & 1) * 64 + ln];
+    rem &= ~(1ull << p);
+    if (ln == p) my_step = k;
+    if (wv == 0 && ln == 0) pv[k] = p;
+    const bool upd = (rem >> ln) & 1ull;
+    const int wn = (k + 1) / CW, cn = (k + 1) % CW;  // owner of the next pivot column (static after unrolling)
+    const bool next_owner = k + 1 < NC && wv == wn;
+    if (next_owner) {
+      const double u = bcast(acol[cn], p);
+      if (upd) acol[cn] = fma(-l, u, acol[cn]);
+      publish_pivot(k + 1, acol[cn], rem, ln, Lb, Pb);
+    }
+    double u[16];
+    bcast_n(CW + 1, acol, 1ull << p, u);
+#pragma unroll
+    for (int c = 0; c <= CW; ++c) {
+      const int j = c < CW ? wv * CW + c : NC;  // the rhs slot: column NC of the last wave
+      const bool live = (c < CW ? (j > k && j < NC && !(next_owner && c == cn)) : rhs_wave);
+      if (upd && live) acol[c] = fma(-l, u[c], acol[c]);
+    }
+  }
+  // U and the reduced right-hand side back to LDS; wave 0 substitutes backwards
+#pragma unroll
+  for (int c = 0; c < CW; ++c) {
+    const int j = wv * CW + c;
+    if (ln < NC && j < NC) Srow[ln * LDR + j] = acol[c];
+  }
+  if (rhs_wave && ln < NC) Srow[ln * LDR + NC] = acol[CW];
+  __syncthreads();
+  if (wv == 0) {
+    double a[NMAX];
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j) a[j] = (ln < NC && j < NC) ? Srow[ln * LDR + j] : 0.0;
+    double b = ln < NC ? Srow[ln * LDR + NC] : 0.0;
+    dz = 0.0;
+#pragma clang loop unroll(full)
+    for (int k = NMAX - 1; k >= 0; --k) {
+      if (k < NC) {
+        const int p = __builtin_amdgcn_readfirstlane(pv[k]);
+        const double xk = bcast(b, p) * rcp_uniform(bcast(a[k], p));  // b_p · (1 / u_kk)
+        if (ln == k) dz = xk;
+        if (my_step < k) b = fma(-a[k], xk, b);
+      }
+    }
+  }
+  return true;
+}
+
+// MW = true (SCHUR only): one 4-wave workgroup per instance (mcpx_nl_solve_schur_mw).  The
+// LU runs on all four waves (lu_solve_mw); wave 0 does the rest, the other waves follow the
+// same control flow from the shared state in LDS (every branch below depends only on LDS
+// contents and lane indices, so all waves take it alike) and write nothing else.
+template <int SOLVER, bool MW = false>
 __device__ __forceinline__ void solve(const KernelArgs& args) {
   constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR, RED = SOLVER == MCPX_LINSOLVE_REDUCED;
   constexpr int NR = rows_of(SOLVER);                 // rows of the factored system
@@ -68,26 +304,33 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   constexpr int LDR = n + 1;  // SCHUR: lane-private LDS rows of S (odd stride: 2-way bank conflicts at most)
   __shared__ double Srow[SCH ? imax(1, n * LDR) : 1];
   __shared__ double sRw[SCH ? MZ : 1], sDi[SCH ? MZ : 1], sRy[SCH ? MZ : 1], sTy[SCH ? MZ : 1];
+  constexpr int WV = MW ? 4 : 1;  // waves per instance
+  static_assert(!MW || SCH, "the multi-wave kernel is the SCHUR one");
+  __shared__ double mwL[MW ? 128 : 1];
+  __shared__ int mwP[MW ? 2 : 1], mwPv[MW ? 64 : 1];
 
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = MW ? __builtin_amdgcn_readfirstlane(tid >> 6) : 0;  // uniform: scalar branches
+  const bool w0 = wv == 0;  // wave 0 owns every write to the shared state
   const int64_t inst = blockIdx.x;
   const double* __restrict__ th = args.theta + inst * args.theta_ld;
   const double tol = args.tol;
   const bool lx = lane < n;
 
-  for (int i = lane; i < BLK; i += 64) blk[i] = 0.0;  // structural zeros, never written again
+  for (int i = tid; i < BLK; i += 64 * WV) blk[i] = 0.0;  // structural zeros, never written again
   // src/solver.jl:39-41, 64-66: x₀ = 0, y₀ = 1, s₀ = 1 unless warm-started
-  if (lx) zs[lane] = args.x0 ? args.x0[inst * n + lane] : 0.0;
+  if (w0 && lx) zs[lane] = args.x0 ? args.x0[inst * n + lane] : 0.0;
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int k = lane + 64 * r;
-    if (k < m) {
+    if (w0 && k < m) {
       zs[n + k] = args.y0 ? args.y0[inst * m + k] : 1.0;
       zs[n + m + k] = args.s0 ? args.s0[inst * m + k] : 1.0;
     }
   }
   __syncthreads();
-  if (lane == 0) mcpx_nl_init(th, blk);
+  if (tid == 0) mcpx_nl_init(th, blk);
 
   double eps = 1.0;                   // :67
   double kkt = __builtin_huge_val();  // :68
@@ -106,7 +349,20 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
     while (kkt > eps && inner < args.max_inner) {              // :75
       // ---- F!, ∇F_z! (:79-81): the generated code, then F = [G; H − s; s⊙y − ϵ] (src/mcp.jl:76-80)
       __syncthreads();
-      if (lane == 0) mcpx_nl_eval(th, zs, blk);
+#if defined(MCPX_NL_EVAL_PARTS) && MCPX_NL_EVAL_PARTS == 4
+      if constexpr (MW) {  // the generated eval's four parts (disjoint outputs), one per wave
+        if (lane == 0) {
+          if (wv == 0) mcpx_nl_eval_p0(th, zs, blk);
+          else if (wv == 1) mcpx_nl_eval_p1(th, zs, blk);
+          else if (wv == 2) mcpx_nl_eval_p2(th, zs, blk);
+          else mcpx_nl_eval_p3(th, zs, blk);
+        }
+      } else if (tid == 0) {
+        mcpx_nl_eval(th, zs, blk);
+      }
+#else
+      if (tid == 0) mcpx_nl_eval(th, zs, blk);
+#endif
       __syncthreads();
       double aF = 0.0;
 #pragma unroll
@@ -117,7 +373,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
           if (i < n) f = blk[OFF_G + i];
           else if (i < n + m) f = blk[OFF_H + (i - n)] - zs[i + m];  // H_k − s_k
           else f = zs[i] * zs[i - m] - eps;                          // s_k·y_k − ϵ
-          Fs[i] = f;
+          if (w0) Fs[i] = f;
           aF = max_nan(aF, fabs(f));
         }
       }
@@ -134,7 +390,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
 #pragma unroll
         for (int r = 0; r < RM; ++r) {
           const int k = lane + 64 * r;
-          if (k < m) {
+          if (w0 && k < m) {
             const double rw = 1.0 / (zs[n + k] + tol);
             const double Di = 1.0 / (tol + zs[n + m + k] * rw);
             const double ry = (-Fs[n + k]) - (Fs[n + m + k] * rw);
@@ -147,7 +403,9 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
         __syncthreads();
         // row i of S = (P + tol·I) − Q D⁻¹ R and rr_i = −F_Gi − Σ_k Q_ik ty_k, k ascending
         // lanes ≥ n hold a copy of row 0: never a pivot row, never updated (lu_solve_rows)
+        // (MW: wave 0 forms the rows into Srow for lu_solve_mw)
         const int i = lx ? lane : 0;
+        if (w0) {
         const double dg = blk[OFF_P + i * n + i] + tol;  // the diagonal entry, one add
         double a[NMAX];
 #pragma unroll
@@ -161,10 +419,11 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
         // (the oracle's chain; at most 3 × 4 terms a row in the lane-change game).  The row
         // indices are per lane, so the row goes through its lane's own LDS row and back.
         const int t0 = lx ? mcpx_nl_qk_ptr[i] : 0, t1 = lx ? mcpx_nl_qk_ptr[i + 1] : 0;
-        if (t1 > t0) {
+        if (MW || t1 > t0) {
           double* row = Srow + i * LDR;
 #pragma unroll
-          for (int j = 0; j < n; ++j) row[j] = a[j];
+          for (int j = 0; j < n; ++j)
+            if (!MW || lx) row[j] = a[j];
           for (int t = t0; t < t1; ++t) {
             const int k = mcpx_nl_qk_idx[t];
             const double q = -blk[OFF_Q + k * n + i], Di = sDi[k];
@@ -174,39 +433,49 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
             }
             rhs = fma(q, sTy[k], rhs);
           }
+          if (MW && lx) row[n] = rhs;
 #pragma unroll
           for (int j = 0; j < n; ++j) a[j] = row[j];
         }
         MCPX_STAMP(1);
-        // LU of S with the previous Newton step's pivot sequence as the guess (the
-        // lane-change game keeps it on 86 % of steps); a missed guess restores the rows
-        // from Srow and factors again with the pivot search.  Bits equal the searched LU.
-        bool spec = have_guess, miss;
-        for (;;) {
-          if (spec && lx) {
+        if constexpr (!MW) {
+        // LU of S (oracle lu_solve_x, reciprocal multipliers) with the previous Newton
+        // step's pivot sequence as the guess (the lane-change game keeps it on 86 % of
+        // steps): the 2-D elimination (lu2d_solve), which reads the rows from Srow in the
+        // guessed order; a missed guess factors the register rows again with the pivot
+        // search.  Bits equal the searched LU.
+        bool miss = true;
+        if (have_guess) {
+          if (lx) {
             double* row = Srow + i * LDR;
 #pragma unroll
             for (int j = 0; j < n; ++j) row[j] = a[j];
             row[n] = rhs;
           }
-          ok = lu_solve_rows_core<NMAX>(a, rhs, opaque(n), lane, dz, piv_guess, spec, miss);
-          if (!miss) break;
-          const double* row = Srow + i * LDR;
-#pragma unroll
-          for (int j = 0; j < NMAX; ++j) a[j] = (j < n) ? row[j] : 0.0;
-          rhs = lx ? row[n] : 0.0;
-          spec = false;
+          __syncthreads();
+          miss = !lu2d_solve<n>(Srow, LDR, lane, piv_guess, dz);
+          ok = !miss;
+        }
+        if (miss) {
+          bool unused;
+          ok = lu_solve_rows_core<NMAX, true>(a, rhs, opaque(n), lane, dz, piv_guess, false, unused);
         }
         have_guess = ok;
+        }  // !MW
+        }  // w0: S formed (and, one-wave, factored)
+        if constexpr (MW) {
+          __syncthreads();  // every row of [S | rr] in Srow
+          ok = lu_solve_mw<n, 4, NMAX>(Srow, LDR, mwL, mwP, mwPv, wv, lane, dz);
+        }
         MCPX_STAMP(2);
         if (ok) {
-          if (lx) dzs[lane] = dz;
+          if (w0 && lx) dzs[lane] = dz;
           __syncthreads();
           // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
 #pragma unroll
           for (int r = 0; r < RM; ++r) {
             const int k = lane + 64 * r;
-            if (k < m) {
+            if (w0 && k < m) {
               double acc = sRy[k];
               for (int t = mcpx_nl_rj_ptr[k]; t < mcpx_nl_rj_ptr[k + 1]; ++t) {  // R's structural nonzeros J(k)
                 const int j = mcpx_nl_rj_idx[t];
@@ -335,16 +604,17 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
       double as = 1.0, ay = 1.0;
       for (int e = 0; e < es; ++e) as *= args.decay;
       for (int e = 0; e < ey; ++e) ay *= args.decay;
-      if (args.alpha_trace && newton < args.trace_len && lane == 0) {
+      if (args.alpha_trace && newton < args.trace_len && tid == 0) {
         uint8_t* tr = args.alpha_trace + ((size_t)inst * args.trace_len + newton) * 2;
         tr[0] = (uint8_t)es;
         tr[1] = (uint8_t)ey;
       }
       // ---- update (:103-105; x moves with α_s) ------------------------------
-      if (lx) zs[lane] = zs[lane] + as * dzs[lane];
+      if constexpr (MW) __syncthreads();  // every wave has read z for its line search
+      if (w0 && lx) zs[lane] = zs[lane] + as * dzs[lane];
 #pragma unroll
       for (int r = 0; r < RM; ++r) {
-        if (own[r]) {
+        if (w0 && own[r]) {
           const int k = lane + 64 * r;
           zs[n + m + k] = sv[r] + as * dsv[r];
           zs[n + k] = yv[r] + ay * dyv[r];
@@ -362,11 +632,11 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
 
   // ---- outputs (:121) -------------------------------------------------------
   __syncthreads();
-  if (lx) args.x[inst * n + lane] = zs[lane];
+  if (w0 && lx) args.x[inst * n + lane] = zs[lane];
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
     const int k = lane + 64 * r;
-    if (k < m) {
+    if (w0 && k < m) {
       args.y[inst * m + k] = zs[n + k];
       args.s[inst * m + k] = zs[n + m + k];
     }
@@ -375,13 +645,13 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
     bool act = false;
     if (lane < m) act = zs[n + imin(lane, MZ - 1)] > zs[n + m + imin(lane, MZ - 1)];
     const uint64_t bits = ballot(act);
-    if (lane == 0) args.active_mask[inst] = bits;
+    if (tid == 0) args.active_mask[inst] = bits;
   }
 #if MCPX_STAMPS
-  if (lane == 0 && args.stamps)
+  if (tid == 0 && args.stamps)
     for (int i = 0; i < 4; ++i) args.stamps[inst * 4 + i] = st_acc[i];
 #endif
-  if (lane == 0) {
+  if (tid == 0) {
     args.kkt_error[inst] = kkt;
     args.eps[inst] = eps;
     args.outer_iters[inst] = outer;
@@ -401,6 +671,8 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
 #define MCPX_NL_CAN_SCHUR                                                                             \
   (!MCPX_NL_HAS_S && MCPX_NL_N >= 1 && MCPX_NL_N <= 64 && MCPX_NL_M <= 128 &&                         \
    MCPX_NL_SCHUR_LDS <= 160 * 1024 - 2048)
+// the 4-wave SCHUR kernel: each wave's columns plus the rhs in one broadcast group (≤ 16)
+#define MCPX_NL_CAN_SCHUR_MW (MCPX_NL_CAN_SCHUR && MCPX_NL_N >= 4 && (MCPX_NL_N + 3) / 4 + 1 <= 16)
 
 // ---- workgroup-per-instance kernels (ipm_wg_impl.hpp) for systems beyond one wave --
 // LDS of solve_instances<…, NV = n + 2m, NS>: z, F, δz (3·NV doubles) and the LU
@@ -441,14 +713,16 @@ constexpr int NVW = imax(1, N);
 // 0, 0, 0}; kernel mask: bit MCPX_LINSOLVE_* = one-wave kernel, bit 3 + MCPX_LINSOLVE_* =
 // workgroup kernel, bit MCPX_MODULE_VJP / MCPX_MODULE_JVP = sensitivity kernels (the
 // VJP factors the (n+m)-dim system of the REDUCED workgroup solver, the JVP the full
-// (n+2m)-dim ∇F_z of the DENSE one: they exist when those fit LDS)
+// (n+2m)-dim ∇F_z of the DENSE one: they exist when those fit LDS), bit MCPX_MODULE_SCHUR_MW =
+// the 4-wave SCHUR kernel mcpx_nl_solve_schur_mw (layout 4)
 extern "C" {
 __device__ int32_t mcpx_nl_meta[12] = {
-    3, MCPX_NL_N, MCPX_NL_M, MCPX_NL_P, MCPX_NL_HAS_S,
+    4, MCPX_NL_N, MCPX_NL_M, MCPX_NL_P, MCPX_NL_HAS_S,
     (MCPX_NL_CAN_REDUCED << MCPX_LINSOLVE_REDUCED) | (MCPX_NL_CAN_DENSE << MCPX_LINSOLVE_DENSE) |
         (MCPX_NL_CAN_SCHUR << MCPX_LINSOLVE_SCHUR) | (MCPX_NL_CAN_WG_REDUCED << (3 + MCPX_LINSOLVE_REDUCED)) |
         (MCPX_NL_CAN_WG_DENSE << (3 + MCPX_LINSOLVE_DENSE)) | (MCPX_NL_CAN_WG_SCHUR << (3 + MCPX_LINSOLVE_SCHUR)) |
-        (MCPX_NL_CAN_WG_REDUCED << MCPX_MODULE_VJP) | (MCPX_NL_CAN_WG_DENSE << MCPX_MODULE_JVP),
+        (MCPX_NL_CAN_WG_REDUCED << MCPX_MODULE_VJP) | (MCPX_NL_CAN_WG_DENSE << MCPX_MODULE_JVP) |
+        (MCPX_NL_CAN_SCHUR_MW << MCPX_MODULE_SCHUR_MW),
     MCPX_NL_SIZE, MCPX_NL_NNZ, MCPX_NL_NNZ_T, 0, 0, 0};
 
 #if MCPX_NL_CAN_WG_REDUCED
@@ -493,6 +767,11 @@ __global__ __launch_bounds__(64) void mcpx_nl_solve_dense(const mcpx::KernelArgs
 #if MCPX_NL_CAN_SCHUR
 __global__ __launch_bounds__(64) void mcpx_nl_solve_schur(const mcpx::KernelArgs args) {
   mcpx::nl::solve<MCPX_LINSOLVE_SCHUR>(args);
+}
+#endif
+#if MCPX_NL_CAN_SCHUR_MW
+__global__ __launch_bounds__(256) void mcpx_nl_solve_schur_mw(const mcpx::KernelArgs args) {
+  mcpx::nl::solve<MCPX_LINSOLVE_SCHUR, true>(args);
 }
 #endif
 }  // extern "C"

@@ -180,7 +180,9 @@ __device__ __forceinline__ int panel_pivot(LuShared<NSMAX>& L, int r, int kk, in
   return p;
 }
 
-template <int NSMAX>
+// RCP: the reciprocal-multiplier arithmetic of oracle lu_solve_x (rcp = 1; the SCHUR step of
+// generated nonlinear modules): l = a_ik · (1 / piv), x_k = b_p · (1 / u_kk).
+template <int NSMAX, bool RCP = false>
 __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns, double* x, LuShared<NSMAX>& L,
                                          int nrhs = 1, double* __restrict__ xout = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -203,6 +205,7 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
       const int pp = panel_pivot(L, r, kk, step);  // barrier inside: the previous update is visible
       const double piv = L.pan[pp * NB + kk];
       if (piv == 0.0) return false;  // the failed linear solve of src/solver.jl:84-88
+      const double rp = RCP ? 1.0 / piv : 1.0;
       if (tid == (pp & (WG - 1))) {  // the owner of the pivot row
         L.ispiv[pp] = 1;
         L.pivpos[kk] = (int16_t)pp;
@@ -212,7 +215,7 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
       for (int q = tid; q < r; q += WG) {
         if (q == pp || L.ispiv[q]) continue;
         double* row = L.pan + q * NB;
-        const double l = row[kk] / piv;
+        const double l = RCP ? row[kk] * rp : row[kk] / piv;
         for (int jj = kk + 1; jj < kb; ++jj) row[jj] = fma(-l, L.pan[pp * NB + jj], row[jj]);
         row[kk] = l;  // a_ik of a remaining row is never read again: keep l_ik there
       }
@@ -362,7 +365,7 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
 #pragma unroll
       for (int c = NB - 1; c >= 0; --c) {
         if (c >= kb) continue;
-        const double t = bj / uj[c];  // lane c: x_{k0+c} = b_p / u_pk
+        const double t = RCP ? bj * (1.0 / uj[c]) : bj / uj[c];  // lane c: x_{k0+c} = b_p / u_pk
         const double xc = __shfl(t, c);
         if (lane == c) x[k0 + c] = xc;
         if (lane < c) bj = fma(-uj[c], xc, bj);
@@ -620,7 +623,9 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
         }
         __syncthreads();
         // ---- LU with partial pivoting (:83-88) ------------------------------------
-        if (!lu_solve<NSMAX>(Am, ld, ns, dzs, S.lu)) {
+        // generated nonlinear modules' SCHUR step: reciprocal multipliers (oracle lu_solve_x)
+        constexpr bool RCP = FAMILY == MCPX_FAMILY_NONLINEAR && SOLVER == MCPX_LINSOLVE_SCHUR;
+        if (!lu_solve<NSMAX, RCP>(Am, ld, ns, dzs, S.lu)) {
           status = 1;
           break;
         }

@@ -101,9 +101,11 @@ int pick_wg_bucket(int N) {
 // *wg: the solve runs on the workgroup-per-instance kernels (ipm_wg_impl.hpp);
 // *nmax: the one-wave kernels' row width, or the workgroup kernels' dimension bucket.
 int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* nmax,
-            const mcpx_module* mod = nullptr, bool* wg = nullptr) {
-  bool wg_local = false;
+            const mcpx_module* mod = nullptr, bool* wg = nullptr, bool* mw = nullptr) {
+  bool wg_local = false, mw_local = false;
   if (!wg) wg = &wg_local;
+  if (!mw) mw = &mw_local;
+  *mw = false;
   if (!d || !p) return fail(MCPX_EINVAL, "desc and params must be non-NULL");
   int64_t pd;
   if (mod) {  // a generated nonlinear module: θ dimension and sizes from its metadata
@@ -126,14 +128,21 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   const int ls = p->linear_solver;
   if (ls != MCPX_LINSOLVE_REDUCED && ls != MCPX_LINSOLVE_DENSE && ls != MCPX_LINSOLVE_SCHUR)
     return fail(MCPX_EINVAL, "unknown linear_solver %d", ls);
-  if (p->kernel != MCPX_KERNEL_AUTO && p->kernel != MCPX_KERNEL_WAVE && p->kernel != MCPX_KERNEL_WORKGROUP)
+  if (p->kernel != MCPX_KERNEL_AUTO && p->kernel != MCPX_KERNEL_WAVE && p->kernel != MCPX_KERNEL_WORKGROUP &&
+      p->kernel != MCPX_KERNEL_MULTIWAVE)
     return fail(MCPX_EINVAL, "unknown kernel selector %d", p->kernel);
   bool wave_ok, wg_ok;
   if (mod) {
     wave_ok = (mod->meta[5] >> ls) & 1;
     wg_ok = (mod->meta[5] >> (3 + ls)) & 1;
+    const bool mw_ok = ls == MCPX_LINSOLVE_SCHUR && ((mod->meta[5] >> MCPX_MODULE_SCHUR_MW) & 1);
+    if (p->kernel == MCPX_KERNEL_MULTIWAVE && !mw_ok)
+      return fail(MCPX_EUNSUPPORTED, "the generated module has no multi-wave kernel for linear_solver=%d", ls);
+    *mw = mw_ok && p->kernel == MCPX_KERNEL_MULTIWAVE;  // measured slower than one wave: opt-in
     *nmax = 0;
   } else {
+    if (p->kernel == MCPX_KERNEL_MULTIWAVE)
+      return fail(MCPX_EUNSUPPORTED, "MCPX_KERNEL_MULTIWAVE is a generated module's SCHUR kernel");
     if (ls == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP)
       return fail(MCPX_EINVAL, "linear_solver=schur needs the QP family (dH/dy = 0)");
     const int N = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : (ls == MCPX_LINSOLVE_REDUCED ? d->n + d->m : d->n);
@@ -144,6 +153,7 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   }
   if (p->kernel == MCPX_KERNEL_WAVE) wg_ok = false;
   if (p->kernel == MCPX_KERNEL_WORKGROUP) wave_ok = false;
+  if (*mw) wave_ok = true;
   if (!wave_ok && !wg_ok) {
     if (mod)
       return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel for linear_solver=%d (n=%d m=%d)",
@@ -189,7 +199,7 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
 }
 
 // ---- generated nonlinear modules ---------------------------------------------
-constexpr int32_t kNLLayout = 3;  // mcpx_nl_meta[0] of csrc/ipm_nl_kernel.hpp
+constexpr int32_t kNLLayout = 4;  // mcpx_nl_meta[0] of csrc/ipm_nl_kernel.hpp
 const char* const kNLKernel[3] = {"mcpx_nl_solve_reduced", "mcpx_nl_solve_dense", "mcpx_nl_solve_schur"};
 
 // `mod` on device `dev` (the current device), loaded on first use.
@@ -207,13 +217,13 @@ int module_on(mcpx_module* mod, int dev, hipModule_t* hm) {
 
 // The module's kernel for linear solver `solver` (one-wave, or the workgroup
 // kernel "<name>_wg") on the current device.
-int nl_function(mcpx_module* mod, int solver, bool wg, hipFunction_t* f) {
+int nl_function(mcpx_module* mod, int solver, bool wg, hipFunction_t* f, bool mw = false) {
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   hipModule_t hm;
   const int rc = module_on(mod, dev, &hm);
   if (rc) return rc;
-  const std::string name = std::string(kNLKernel[solver]) + (wg ? "_wg" : "");
+  const std::string name = std::string(kNLKernel[solver]) + (wg ? "_wg" : (mw ? "_mw" : ""));
   if (hipModuleGetFunction(f, hm, name.c_str()) != hipSuccess)
     return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel", name.c_str());
   return MCPX_OK;
@@ -322,20 +332,21 @@ int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const d
 
 int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                   const double* s0, const mcpx_out* o, mcpx::KernelArgs a, int nmax, hipStream_t st,
-                  mcpx_module* mod = nullptr, bool wg = false) {
+                  mcpx_module* mod = nullptr, bool wg = false, bool mw = false) {
   if (wg) return launch_wg(d, theta, x0, y0, s0, o, a, nmax, st, mod);
   hipFunction_t nlf = nullptr;  // generated module: its kernel, launched by hipModuleLaunchKernel
   if (mod) {
-    const int rc = nl_function(mod, a.solver, false, &nlf);
+    const int rc = nl_function(mod, a.solver, false, &nlf, mw);
     if (rc) return rc;
   }
+  const unsigned threads = mw ? 256 : 64;  // the multi-wave SCHUR kernel: 4 waves per instance
   const int64_t CH = (int64_t)1 << 30;
   for (int64_t b0 = 0; b0 < d->batch; b0 += CH) {
     const int64_t nb = std::min(CH, d->batch - b0);
     set_chunk(a, d, theta, x0, y0, s0, o, b0);
     if (mod) {
       void* params[] = {&a};
-      HIP_TRY(hipModuleLaunchKernel(nlf, (unsigned)nb, 1, 1, 64, 1, 1, 0, st, params, nullptr));
+      HIP_TRY(hipModuleLaunchKernel(nlf, (unsigned)nb, 1, 1, threads, 1, 1, 0, st, params, nullptr));
     } else {
       HIP_TRY(launch(nmax, a, nb, st));
     }
@@ -499,8 +510,8 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   if (rc) return rc;
   mcpx::KernelArgs a;
   int nmax;
-  bool wg = false;
-  if ((rc = prepare(d, prm, &a, &nmax, mod, &wg))) return rc;
+  bool wg = false, mw = false;
+  if ((rc = prepare(d, prm, &a, &nmax, mod, &wg, &mw))) return rc;
   const int n = d->n, m = d->m;
   if (m > 64 && o->active_mask) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
   PipeLease lease;
@@ -562,7 +573,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
     od.trace_len = want_tr ? o->trace_len : 0;
     mcpx_desc dd = *d;
     dd.batch = cn;
-    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, cs, mod, wg))) return rc;
+    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, cs, mod, wg, mw))) return rc;
     HIP_TRY(hipEventRecord(P->consumed[k], cs));
   }
   HIP_TRY(hipStreamSynchronize(us));
@@ -912,8 +923,8 @@ int solve_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta,
                       void* stream) {
   mcpx::KernelArgs a;
   int nmax;
-  bool wg = false;
-  int rc = prepare(d, prm, &a, &nmax, mod, &wg);
+  bool wg = false, mw = false;
+  int rc = prepare(d, prm, &a, &nmax, mod, &wg, &mw);
   if (rc) return rc;
   if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
   if (d->batch == 0) return MCPX_OK;
@@ -921,7 +932,7 @@ int solve_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta,
   if (o->active_mask && d->m > 64) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
   int dev = 0;
   if ((rc = current_device(&dev))) return rc;
-  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod, wg);
+  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod, wg, mw);
 }
 
 // mcpx_solve_vjp_batch_device: the solve kernels with the pullback in their epilogue

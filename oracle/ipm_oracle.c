@@ -225,8 +225,11 @@ static double family_row(int family, int n, int m, const double* th, const doubl
 }
 
 /* ---- dense LU with partial pivoting on [J | b]; returns 0 ok, 1 singular ---- */
-static int lu_solve(int N, double* J /* N×N row-major, destroyed */, double* b /* destroyed */,
-                    double* dz, int* remaining, int* step_of, int* prow) {
+/* rcp = 1 (the SCHUR step of generated nonlinear modules): multipliers a_ik · (1 / piv) and
+ * back substitution x_k = b_p · (1 / u_kk), one correctly rounded reciprocal per pivot — the
+ * arithmetic of the kernels' 2-D Gauss elimination (csrc/ipm_nl_kernel.hpp, lu2d_solve). */
+static int lu_solve_x(int N, double* J /* N×N row-major, destroyed */, double* b /* destroyed */,
+                      double* dz, int* remaining, int* step_of, int* prow, int rcp) {
   for (int i = 0; i < N; ++i) remaining[i] = 1;
   for (int k = 0; k < N; ++k) {
     int best = -1;
@@ -245,17 +248,18 @@ static int lu_solve(int N, double* J /* N×N row-major, destroyed */, double* b 
     step_of[best] = k;
     prow[k] = best;
     const double* u = J + (size_t)best * N;
+    const double rp = 1.0 / piv;
     for (int i = 0; i < N; ++i) {
       if (!remaining[i]) continue;
       double* a = J + (size_t)i * N;
-      const double l = a[k] / piv;
+      const double l = rcp ? a[k] * rp : a[k] / piv;
       for (int j = k + 1; j < N; ++j) a[j] = fma(-l, u[j], a[j]);
       b[i] = fma(-l, b[best], b[i]);
     }
   }
   for (int k = N - 1; k >= 0; --k) {
     const int p = prow[k];
-    const double xk = b[p] / J[(size_t)p * N + k];
+    const double xk = rcp ? b[p] * (1.0 / J[(size_t)p * N + k]) : b[p] / J[(size_t)p * N + k];
     dz[k] = xk;
     for (int i = 0; i < N; ++i)
       if (step_of[i] < k) b[i] = fma(-J[(size_t)i * N + k], xk, b[i]);
@@ -287,6 +291,10 @@ static int gj_spd_solve(int n, double* S /* n×n row-major, destroyed */, double
   }
   for (int i = 0; i < n; ++i) dz[i] = b[i] / S[(size_t)i * n + i];
   return 0;
+}
+
+static int lu_solve(int N, double* J, double* b, double* dz, int* remaining, int* step_of, int* prow) {
+  return lu_solve_x(N, J, b, dz, remaining, step_of, prow, 0);
 }
 
 /* first e in [0, n_trials) with no violation, or -1 (the NaN of src/solver.jl:131) */
@@ -449,7 +457,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           memcpy(w->bs, w->b, sizeof(double) * n);
           spd_ok = gj_spd_solve(n, w->Js, w->bs, w->dz) == 0;
         }
-        if (!spd_ok && lu_solve(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
+        if (!spd_ok && lu_solve_x(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow, nl != NULL)) {
           status = MCPX_STATUS_FAILED;
           break;
         }

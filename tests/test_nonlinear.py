@@ -129,14 +129,17 @@ def test_generated_modules_compile(lane):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B", [1, 257])
-def test_gpu_lane_change_bit_exact(gpu, lane, oracle_lib, B):
+@pytest.mark.parametrize("kernel", ["multiwave", "auto"])
+def test_gpu_lane_change_bit_exact(gpu, lane, oracle_lib, B, kernel):
+    """multiwave = the 4-wave SCHUR kernel (mcpx_nl_solve_schur_mw), auto = the one-wave kernel."""
     from mcp_amd.batch import solve_batch
 
     mcp = lane.mcp
+    assert mcp.module().has_schur_mw
     th = lane.example_parameters()[None] if B == 1 else lane.generate_random_parameter(np.random.default_rng(7), B)
     tp, x0 = mcp.theta_map(th), lane.initial_guess(th)
     got = solve_batch(_abi.FAMILY_NONLINEAR, 40, 50, tp, x0=x0, linear_solver="schur", trace_len=TRACE,
-                      module=mcp.module())
+                      module=mcp.module(), kernel=kernel)
     ref = oracle_lib.solve_batch_nl(mcp.nl, tp, x0=x0, linear_solver="schur", trace_len=TRACE, nthreads=8)
     assert_parity(got, ref)
     if B == 1:
@@ -181,6 +184,9 @@ def test_gpu_module_rejects_missing_solver(gpu):
     mcp = cubic_mcp()
     with pytest.raises(MCPXError):
         solve_batch(_abi.FAMILY_NONLINEAR, 1, 1, _cubic_theta(4), linear_solver="schur", module=mcp.module())
+    with pytest.raises(MCPXError):  # no multi-wave kernel for n < 4
+        solve_batch(_abi.FAMILY_NONLINEAR, 1, 1, _cubic_theta(4), linear_solver="reduced", module=mcp.module(),
+                    kernel="multiwave")
 
 
 @pytest.mark.gpu
@@ -199,7 +205,8 @@ def test_gpu_lane_change_api_device_path(gpu, lane, oracle_lib):
 
 
 @pytest.mark.gpu
-def test_gpu_lane_change_c4_batch_and_edge_inputs(gpu, lane, oracle_lib):
+@pytest.mark.parametrize("kernel", ["multiwave", "wave"])
+def test_gpu_lane_change_c4_batch_and_edge_inputs(gpu, lane, oracle_lib, kernel):
     """The BASELINE C4 batch itself (1,024 games of the bench's θ stream, 45-50 of which run
     all 931 Newton steps) plus games with NaN / Inf / huge / zeroed parameters, bit-exact vs
     the oracle.  Exercises the guessed-pivot LU of mcpx_nl_solve_schur on every path: guesses
@@ -221,7 +228,8 @@ def test_gpu_lane_change_c4_batch_and_edge_inputs(gpu, lane, oracle_lib):
     edge[7, 9] = 1e6
     th = np.concatenate([th, edge])
     tp = np.ascontiguousarray(mcp.theta_map(th))
-    got = solve_batch(_abi.FAMILY_NONLINEAR, 40, 50, tp, linear_solver="schur", trace_len=TRACE, module=mcp.module())
+    got = solve_batch(_abi.FAMILY_NONLINEAR, 40, 50, tp, linear_solver="schur", trace_len=TRACE, module=mcp.module(),
+                      kernel=kernel)
     ref = oracle_lib.solve_batch_nl(mcp.nl, tp, linear_solver="schur", trace_len=TRACE, nthreads=8)
     assert_parity(got, ref)
     assert (ref["newton_iters"][:1024] == 931).sum() >= 30  # the tail really ran

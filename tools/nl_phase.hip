@@ -1,6 +1,6 @@
 // Diagnostic: per-phase s_memtime cycles of a generated nonlinear module's one-wave kernel
 // (module built with -DMCPX_STAMPS=1; see tools/nl_phase.py, which writes θ and runs this).
-//   nl_phase <module.hsaco> <kernel> <theta.bin> n m p B
+//   nl_phase <module.hsaco> <kernel> <theta.bin> n m p B [threads per instance: 64, or 256 for _mw]
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
@@ -12,6 +12,7 @@ int main(int argc, char** argv) {
   if (argc < 8) { fprintf(stderr, "usage\n"); return 2; }
   const char *mod = argv[1], *kname = argv[2], *thf = argv[3];
   const int n = atoi(argv[4]), m = atoi(argv[5]), p = atoi(argv[6]), B = atoi(argv[7]);
+  const unsigned threads = argc > 8 ? (unsigned)atoi(argv[8]) : 64u;
   std::vector<double> th((size_t)B * p);
   FILE* f = fopen(thf, "rb");
   if (!f || fread(th.data(), 8, th.size(), f) != th.size()) { fprintf(stderr, "theta read failed\n"); return 2; }
@@ -44,7 +45,7 @@ int main(int argc, char** argv) {
   float ms = 0;
   for (int rep = 0; rep < 2; ++rep) {
     (void)hipEventRecord(e0, 0);
-    if (hipModuleLaunchKernel(K, B, 1, 1, 64, 1, 1, 0, 0, nullptr, cfg) != hipSuccess) { fprintf(stderr, "launch failed\n"); return 2; }
+    if (hipModuleLaunchKernel(K, B, 1, 1, threads, 1, 1, 0, 0, nullptr, cfg) != hipSuccess) { fprintf(stderr, "launch failed\n"); return 2; }
     (void)hipEventRecord(e1, 0);
     (void)hipDeviceSynchronize();
     (void)hipEventElapsedTime(&ms, e0, e1);
