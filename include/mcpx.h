@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define MCPX_VERSION 10500 /* 1.5.0 */
+#define MCPX_VERSION 10600 /* 1.6.0 */
 
 /* error codes */
 #define MCPX_OK 0
@@ -65,6 +65,11 @@ extern "C" {
 /* per-instance status (reference: :solved / :failed, src/solver.jl:69,86,98,118) */
 #define MCPX_STATUS_SOLVED 0
 #define MCPX_STATUS_FAILED 1
+/* mcpx_out.fail_reason bits: the events behind the reference's `verbose` warnings
+ * (src/solver.jl), each set when it happened at least once during the solve */
+#define MCPX_FAIL_LINSOLVE 1u   /* a Newton system was singular, a zero pivot (:84-88) */
+#define MCPX_FAIL_LINESEARCH 2u /* the fraction-to-the-boundary line search gave NaN (:93-99) */
+#define MCPX_FAIL_MAX_OUTER 4u  /* outer_iters reached max_outer_iters (:117-119) */
 
 #define MCPX_FAMILY_QP 0
 #define MCPX_FAMILY_AFFINE 1
@@ -151,7 +156,9 @@ typedef struct mcpx_desc {
  * (NULL = not wanted): newton_iters (total Newton steps taken),
  * active_mask (bit k of word b*W + k/64 set iff y_k > s_k at return, W = max(1, ⌈m/64⌉)),
  * alpha_trace (per accepted Newton step two bytes (e_s, e_y): α = decay^e;
- * at most trace_len steps recorded per instance). */
+ * at most trace_len steps recorded per instance), fail_reason (MCPX_FAIL_* bits of the
+ * failure events seen; status is FAILED iff MCPX_FAIL_MAX_OUTER is set or the last
+ * outer iteration ended in one of the other two). */
 typedef struct mcpx_out {
   double* x;            /* [B*n] */
   double* y;            /* [B*m] */
@@ -165,6 +172,7 @@ typedef struct mcpx_out {
   uint8_t* alpha_trace;   /* [B*trace_len*2] or NULL */
   int32_t trace_len;
   int32_t pad_;
+  uint8_t* fail_reason;   /* [B] or NULL */
 } mcpx_out;
 
 int mcpx_version(void);

@@ -10,6 +10,10 @@ MCPX_EUNSUPPORTED = -4
 
 STATUS_SOLVED = 0
 STATUS_FAILED = 1
+# fail_reason bits (include/mcpx.h MCPX_FAIL_*)
+FAIL_LINSOLVE = 1
+FAIL_LINESEARCH = 2
+FAIL_MAX_OUTER = 4
 
 FAMILY_QP = 0
 FAMILY_AFFINE = 1
@@ -80,6 +84,7 @@ class Out(C.Structure):
         ("alpha_trace", C.c_void_p),
         ("trace_len", C.c_int32),
         ("pad_", C.c_int32),
+        ("fail_reason", C.c_void_p),
     ]
 
 

@@ -596,9 +596,12 @@ def solve(solver_type, mcp=None, θ=None, *, x0=None, y0=None, s0=None, tol=1e-4
     B = tp.shape[0]
     r = solve_batch(mcp.family, n, m, tp, x0=x0, y0=y0, s0=s0, params=prm, num_devices=num_devices,
                     trace_len=trace_len, module=mcp.module() if mcp.nl is not None else None)
-    if verbose:
-        for b in np.nonzero(r["status"] != 0)[0][:16]:
-            warnings.warn(f"instance {b}: Newton linear solve or line search failed "
+    if verbose:  # the warnings of src/solver.jl:85,97 from the per-instance failure events
+        fr = r["fail_reason"]
+        for b in np.nonzero(fr & (_abi.FAIL_LINSOLVE | _abi.FAIL_LINESEARCH))[0][:16]:
+            what = [w for bit, w in ((_abi.FAIL_LINSOLVE, "Linear solve failed"),
+                                     (_abi.FAIL_LINESEARCH, "Linesearch failed")) if fr[b] & bit]
+            warnings.warn(f"instance {b}: {'; '.join(what)}. Exiting prematurely "
                           f"(outer_iters={r['outer_iters'][b]}, kkt_error={r['kkt_error'][b]:.3e})")
     # aliasing of caller-supplied warm starts (src/solver.jl:64-66)
     for key, w in (("x", x0), ("y", y0), ("s", s0)):

@@ -73,6 +73,7 @@ def alloc_host_outputs(B: int, n: int, m: int, trace_len: int = 0) -> dict:
         newton_iters=np.zeros(B, np.int32),
         active_mask=np.zeros((B, words), np.uint64) if m <= 64 else None,
         alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+        fail_reason=np.zeros(B, np.uint8),
     )
     return r
 
@@ -102,11 +103,13 @@ def solve_batch(family: int, n: int, m: int, theta, *, x0=None, y0=None, s0=None
             newton_iters=np.empty(B, np.int32),
             active_mask=np.empty((B, words), np.uint64) if m <= 64 else None,
             alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+            fail_reason=np.empty(B, np.uint8),
         )
+    fr = r.get("fail_reason")
     out = _abi.Out(_ptr(r["x"]), _ptr(r["y"]), _ptr(r["s"]), _ptr(r["kkt_error"]), _ptr(r["eps"]),
                    _ptr(r["outer_iters"]), _ptr(r["status"]), _ptr(r["newton_iters"]),
                    _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
-                   int(trace_len), 0)
+                   int(trace_len), 0, _ptr(fr) if fr is not None else None)
     desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
     if module is not None:  # MCPX_FAMILY_NONLINEAR: the problem's generated code object
         check(lib().mcpx_solve_batch_module(module.handle, C.byref(desc), _ptr(theta), _ptr(x0), _ptr(y0),
@@ -149,6 +152,7 @@ def alloc_device_outputs(B: int, n: int, m: int, device, trace_len: int = 0, new
         newton_iters=torch.empty(B, **i32) if newton else None,
         active_mask=torch.empty(B, dtype=torch.int64, device=device) if (active and m <= 64) else None,
         alpha_trace=torch.full((B, trace_len, 2), 254, dtype=torch.uint8, device=device) if trace_len > 0 else None,
+        fail_reason=torch.empty(B, dtype=torch.uint8, device=device),
     )
 
 
@@ -175,7 +179,7 @@ def solve_batch_device(family: int, n: int, m: int, theta, out: dict | None = No
     tl = 0 if out.get("alpha_trace") is None else out["alpha_trace"].shape[1]
     o = _abi.Out(dp(out["x"]), dp(out["y"]), dp(out["s"]), dp(out["kkt_error"]), dp(out["eps"]),
                  dp(out["outer_iters"]), dp(out["status"]), dp(out.get("newton_iters")),
-                 dp(out.get("active_mask")), dp(out.get("alpha_trace")), int(tl), 0)
+                 dp(out.get("active_mask")), dp(out.get("alpha_trace")), int(tl), 0, dp(out.get("fail_reason")))
     prm = _params(params, **kw)
     desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
     st = stream if stream is not None else torch.cuda.current_stream(theta.device)
@@ -311,7 +315,7 @@ def solve_vjp_batch_device(family: int, n: int, m: int, theta, out: dict | None 
     tl = 0 if out.get("alpha_trace") is None else out["alpha_trace"].shape[1]
     o = _abi.Out(dp(out["x"]), dp(out["y"]), dp(out["s"]), dp(out["kkt_error"]), dp(out["eps"]),
                  dp(out["outer_iters"]), dp(out["status"]), dp(out.get("newton_iters")),
-                 dp(out.get("active_mask")), dp(out.get("alpha_trace")), int(tl), 0)
+                 dp(out.get("active_mask")), dp(out.get("alpha_trace")), int(tl), 0, dp(out.get("fail_reason")))
     cot = _abi.Cotangent(float(ct[0]), float(ct[1]), float(ct[2]), _dev_f64(bx, "bx"), _dev_f64(by, "by"),
                          _dev_f64(bs, "bs"))
     prm = _params(params, **kw)

@@ -367,6 +367,25 @@ class NLSystem:
                             [x for r in rows for x in r])
         return csr(qk), csr(rj)
 
+    def schur_entries(self):
+        """The entries of [S | rr] the SCHUR elimination changes beyond P + tol·I and −F_G:
+        (position i·(n+1) + j, [k ascending]) for each structural nonzero (i, j) of Q D⁻¹ R
+        (k ∈ K(i) with j ∈ J(k)) and (i·(n+1) + n, K(i)) for each rr_i with K(i) ≠ ∅,
+        sorted by position.  The one-wave SCHUR kernel gives each entry's fma chain to one
+        lane (csrc/ipm_nl_kernel.hpp schur_form_entries)."""
+        (qp, qi), (rp, ri) = self.structure()
+        n, ldr, out = self.n, self.n + 1, []
+        for i in range(n):
+            K = qi[qp[i]:qp[i + 1]]
+            cols = {}
+            for k in K:
+                for j in ri[rp[k]:rp[k + 1]]:
+                    cols.setdefault(j, []).append(k)
+            out += [(i * ldr + j, cols[j]) for j in sorted(cols)]
+            if K:
+                out.append((i * ldr + n, list(K)))
+        return out
+
     def theta_structure(self):
         """Structural nonzeros of ∇F_θ's G/H rows: (ptr, idx) CSR by θ column (rows i
         ascending) and by row (θ columns t ascending)."""
@@ -390,6 +409,16 @@ class NLSystem:
                       "  (void)th;", "  (void)z;", "  (void)blk;", *body, "}"]
         (qp, qi), (rp, ri) = self.structure()
         (tcp, tci), (trp, tri) = self.theta_structure()
+        se = self.schur_entries()
+        se_er = max(1, -(-len(se) // 64))
+        se_kt = max([1] + [len(ks) for _, ks in se])
+        se_pos = [-1] * (64 * se_er)
+        se_k = [-1] * (64 * se_er * se_kt)
+        for e, (pos, ks) in enumerate(se):
+            r, ln = divmod(e, 64)
+            se_pos[e] = pos
+            for t, k in enumerate(ks):
+                se_k[(r * se_kt + t) * 64 + ln] = k
         arr = lambda name, v: f"MCPX_NL_TABLE int32_t {name}[{max(len(v), 1)}] = {{{', '.join(map(str, v)) or '0'}}};"
         return "\n".join([
             "/* generated by mcp_amd/codegen.py — do not edit */",
@@ -407,6 +436,12 @@ class NLSystem:
             arr("mcpx_nl_qk_idx", qi),
             arr("mcpx_nl_rj_ptr", rp),
             arr("mcpx_nl_rj_idx", ri),
+            "/* entries of [S | rr] beyond P + tol·I and −F_G (schur_entries): slot e = lane + 64r holds",
+            "   position mcpx_nl_se_pos[e] (−1: none) and its k ascending, mcpx_nl_se_k[(r·KT + t)·64 + lane] */",
+            f"#define MCPX_NL_SE_ER {se_er}",
+            f"#define MCPX_NL_SE_KT {se_kt}",
+            arr("mcpx_nl_se_pos", se_pos),
+            arr("mcpx_nl_se_k", se_k),
             "/* structural nonzeros of ∇F_θ (G/H rows): rows of column t, columns of row i (CSR) */",
             arr("mcpx_nl_tc_ptr", tcp),
             arr("mcpx_nl_tc_idx", tci),

@@ -1,17 +1,22 @@
 // Workgroup-per-instance kernels of the QP and affine families (ipm_wg_impl.hpp):
-// MCPX_LINSOLVE_REDUCED / _DENSE at vector dimension buckets 128 … 768.
+// MCPX_LINSOLVE_REDUCED / _DENSE at vector dimension buckets 128 … 768.  A system of at
+// most MCPX_VR_MAX rows in a larger bucket (REDUCED at KKT 256: n + m = 192) takes the
+// instance whose LU holds the matrix in registers (NS = MCPX_VR_MAX, lu_vr.hpp).
 #include "ipm_wg_impl.hpp"
 
 namespace mcpx {
 
-template <int FAMILY, int SOLVER, int NV>
+template <int FAMILY, int SOLVER, int NV, int NS = NV>
 __global__ __launch_bounds__(wg::kThreads) void ipm_wg_kernel_t(const wg::WgArgs args) {
-  wg::solve_instances<FAMILY, SOLVER, NV, NV, wg::NoGen>(args);
+  wg::solve_instances<FAMILY, SOLVER, NV, NS, wg::NoGen>(args);
 }
 
 namespace {
 template <int FAMILY, int SOLVER>
-const void* pick(int nv) {
+const void* pick(int nv, int ns) {
+#if MCPX_VR_MAX > 0
+  if (nv == 256 && ns <= MCPX_VR_MAX) return (const void*)&ipm_wg_kernel_t<FAMILY, SOLVER, 256, MCPX_VR_MAX>;
+#endif
   switch (nv) {
     case 128: return (const void*)&ipm_wg_kernel_t<FAMILY, SOLVER, 128>;
     case 256: return (const void*)&ipm_wg_kernel_t<FAMILY, SOLVER, 256>;
@@ -22,21 +27,21 @@ const void* pick(int nv) {
 }
 }  // namespace
 
-const void* ipm_wg_kernel(int family, int solver, int nv) {
+const void* ipm_wg_kernel(int family, int solver, int nv, int ns) {
   const bool qp = family == MCPX_FAMILY_QP;
   if (family != MCPX_FAMILY_QP && family != MCPX_FAMILY_AFFINE) return nullptr;
   switch (solver) {
     case MCPX_LINSOLVE_REDUCED:
-      return qp ? pick<MCPX_FAMILY_QP, MCPX_LINSOLVE_REDUCED>(nv) : pick<MCPX_FAMILY_AFFINE, MCPX_LINSOLVE_REDUCED>(nv);
+      return qp ? pick<MCPX_FAMILY_QP, MCPX_LINSOLVE_REDUCED>(nv, ns) : pick<MCPX_FAMILY_AFFINE, MCPX_LINSOLVE_REDUCED>(nv, ns);
     case MCPX_LINSOLVE_DENSE:
-      return qp ? pick<MCPX_FAMILY_QP, MCPX_LINSOLVE_DENSE>(nv) : pick<MCPX_FAMILY_AFFINE, MCPX_LINSOLVE_DENSE>(nv);
+      return qp ? pick<MCPX_FAMILY_QP, MCPX_LINSOLVE_DENSE>(nv, ns) : pick<MCPX_FAMILY_AFFINE, MCPX_LINSOLVE_DENSE>(nv, ns);
     default:
       return nullptr;
   }
 }
 
-hipError_t launch_ipm_wg(int family, int solver, int nv, const wg::WgArgs& a, int grid, hipStream_t st) {
-  const void* k = ipm_wg_kernel(family, solver, nv);
+hipError_t launch_ipm_wg(int family, int solver, int nv, int ns, const wg::WgArgs& a, int grid, hipStream_t st) {
+  const void* k = ipm_wg_kernel(family, solver, nv, ns);
   if (!k) return hipErrorInvalidValue;
   void* params[] = {(void*)&a};
   return hipLaunchKernel(k, dim3((unsigned)grid), dim3(wg::kThreads), params, 0, st);

@@ -29,6 +29,7 @@ struct KernelArgs {
   int32_t* newton_iters;
   uint64_t* active_mask;
   uint8_t* alpha_trace;
+  uint8_t* fail_reason;  // MCPX_FAIL_* bits per instance, or NULL
   uint64_t* stamps;  // diagnostic builds only (MCPX_STAMPS); NULL otherwise
   int32_t trace_len;
   int32_t n, m;

@@ -141,17 +141,22 @@ __device__ __forceinline__ double wave_max_nonneg(double v) {
 // same chain without them (7 instructions) gives the same bits; other b (0,
 // subnormal, huge, Inf, NaN) take the full division.  The test is on the SGPR
 // copy of b, so the branch is scalar.
-__device__ __forceinline__ double rcp_uniform(double b) {
+__device__ __forceinline__ bool rcp_fast_ok(double b) {
   const uint32_t e = ((uint32_t)__double2hiint(b) >> 20) & 0x7ffu;  // biased exponent
-  if (__builtin_expect(e - 523u <= 1000u, 1)) {
-    double y = __builtin_amdgcn_rcp(b);
-    double t = fma(-b, y, 1.0);
-    y = fma(y, t, y);
-    t = fma(-b, y, 1.0);
-    y = fma(y, t, y);
-    t = fma(-b, y, 1.0);  // remainder of the quotient 1·y
-    return fma(t, y, y);
-  }
+  return e - 523u <= 1000u;
+}
+// The 7-instruction chain alone: == 1.0 / b whenever rcp_fast_ok(b).
+__device__ __forceinline__ double rcp_fast(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  double t = fma(-b, y, 1.0);
+  y = fma(y, t, y);
+  t = fma(-b, y, 1.0);
+  y = fma(y, t, y);
+  t = fma(-b, y, 1.0);  // remainder of the quotient 1·y
+  return fma(t, y, y);
+}
+__device__ __forceinline__ double rcp_uniform(double b) {
+  if (__builtin_expect(rcp_fast_ok(b), 1)) return rcp_fast(b);
   return 1.0 / b;
 }
 
@@ -958,6 +963,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   int status = 0;                      // :69
   int outer = 1;                       // :70
   int newton = 0;
+  unsigned reason = 0;  // MCPX_FAIL_* events
 #if MCPX_STAMPS
   uint64_t st_acc[MCPX_NSTAMP] = {};
   uint64_t st_last = __builtin_amdgcn_s_memtime();
@@ -1061,6 +1067,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       MCPX_STAMP(3);
       if (!ok) {
         status = 1;
+        reason |= MCPX_FAIL_LINSOLVE;
         break;
       }
       if constexpr (SCH) {  // δy_k = (ry_k − Σ_j A_kj δx_j) / D_k
@@ -1101,6 +1108,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       const int ey = (~vy) ? lowest_lane(~vy) : 64;
       if (es >= args.n_trials || ey >= args.n_trials) {  // α = NaN
         status = 1;
+        reason |= MCPX_FAIL_LINESEARCH;
         break;
       }
       double as = 1.0, ay = 1.0;
@@ -1131,7 +1139,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
     eps *= (status == 0) ? args.tight[inner] : args.loose[inner];  // :111-113
     ++outer;                                                        // :114
   }
-  if (outer == args.max_outer) status = 1;  // :117-119
+  if (outer == args.max_outer) {  // :117-119
+    status = 1;
+    reason |= MCPX_FAIL_MAX_OUTER;
+  }
 
   // ---- outputs (:121) -----------------------------------------------------
   const int n = n0, m = m0;
@@ -1165,6 +1176,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
     args.outer_iters[inst] = outer;
     args.status[inst] = status;
     if (args.newton_iters) args.newton_iters[inst] = newton;
+    if (args.fail_reason) args.fail_reason[inst] = (uint8_t)reason;
   }
   if constexpr (FUSE > 0) {
     static_assert(RED && FAMILY == MCPX_FAMILY_QP, "the fused pullback follows the QP REDUCED / SCHUR lane layout");

@@ -73,27 +73,33 @@ struct Lu2d {
   static constexpr int NJ = (NM + 15) / 16, NCB = (NM + 3) / 4;
 };
 
+// Step K with one step of lookahead: `piv` (uniform) and `col` (column K by position,
+// from ds_bpermute) were fetched by step K − 1 right after it updated column K, so their
+// LDS latency hides behind the rest of that step's update.  Step K updates the column
+// block of column K + 1 first, fetches pivot K + 1 and its column, then updates the other
+// blocks.  Each entry still takes the same fma in the same order.  1 / piv is the
+// uniform fast reciprocal with no branch: a pivot that is zero, NaN or outside its exact
+// range only sets `bad`, the remaining steps run on (discarded) values, and the caller
+// falls back to the searched LU.
 template <int NM, int K>
 __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
                                           const int (&pv)[Lu2d<NM>::NJ], int pkk, int ln, uint32_t& viol,
-                                          double& rpv, bool& sing) {
+                                          double& rpv, bool& bad, double& piv, double (&col)[Lu2d<NM>::NJ]) {
   constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
-  constexpr int Jk = K >> 4, Rk = K & 15, Qk = K & 3, Ck = K >> 2;
+  constexpr int Jk = K >> 4, Rk = K & 15;
+  constexpr bool NX = K + 1 < NM;  // a next pivot to fetch
+  constexpr int Jn = (K + 1) >> 4, Rn = (K + 1) & 15, Qn = (K + 1) & 3, Cn = (K + 1) >> 2;
   __builtin_amdgcn_sched_barrier(0);  // one step at a time: no step's uniform values hoisted ahead
   const int lc = ln & 15;
-  const double piv = bcast(acc[Jk][Ck], 16 * Qk + Rk);
-  if (!(fabs(piv) > 0.0)) {
-    sing = true;
-    return;
-  }
-  const double rp = rcp_uniform(piv);
+  bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
+  const double rp = rcp_fast(piv);
   if (ln == K) rpv = rp;
   const int64_t kp = (int64_t)((uint64_t)__double_as_longlong(piv) & 0x7fffffffffffffffull);
   double nlm[NJ];
 #pragma unroll
   for (int J = 0; J < NJ; ++J) {
     if (J < Jk) continue;
-    const double v = bperm_f64_addr(acc[J][Ck], (16 * Qk + lc) << 2);  // a_qk of position q = lc + 16J
+    const double v = col[J];  // a_qk of position q = lc + 16J
     const int q = lc + 16 * J;
     const bool remq = (q > K) & (q < NM);
     const int64_t kq = (int64_t)((uint64_t)__double_as_longlong(v) & 0x7fffffffffffffffull);
@@ -101,19 +107,29 @@ __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::
     viol |= (uint32_t)((uint64_t)d >> 63) & (uint32_t)remq;
     nlm[J] = remq ? -(v * rp) : 0.0;
   }
+  if constexpr (NX) {  // column block of column K + 1, then pivot K + 1 and its column
+#pragma unroll
+    for (int J = 0; J < NJ; ++J)
+      if (J > Jk) fmac_row_bcast<Rk, false>(acc[J][Cn], acc[Jk][Cn], nlm[J]);
+    fmac_row_bcast_self<Rk, false>(acc[Jk][Cn], nlm[Jk]);
+    piv = bcast(acc[Jn][Cn], 16 * Qn + Rn);
+#pragma unroll
+    for (int J = 0; J < NJ; ++J)
+      if (J >= Jn) col[J] = bperm_f64_addr(acc[J][Cn], (16 * Qn + lc) << 2);
+  }
 #pragma unroll
   for (int J = 0; J < NJ; ++J) {
     if (J <= Jk) continue;
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
-      if (4 * c + 3 <= K) continue;
+      if (4 * c + 3 <= K || (NX && c == Cn)) continue;
       fmac_row_bcast<Rk, false>(acc[J][c], acc[Jk][c], nlm[J]);
     }
     fmac_row_bcast<Rk, false>(rh[J], rh[Jk], nlm[J]);
   }
 #pragma unroll
   for (int c = 0; c < NCB; ++c) {
-    if (4 * c + 3 <= K) continue;
+    if (4 * c + 3 <= K || (NX && c == Cn)) continue;
     fmac_row_bcast_self<Rk, false>(acc[Jk][c], nlm[Jk]);
   }
   fmac_row_bcast_self<Rk, false>(rh[Jk], nlm[Jk]);
@@ -123,8 +139,13 @@ template <int NM, int... K>
 __device__ __forceinline__ void lu2d_steps(std::integer_sequence<int, K...>,
                                            double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
                                            const int (&pv)[Lu2d<NM>::NJ], int pk, int ln, uint32_t& viol, double& rpv,
-                                           bool& sing) {
-  ((sing ? void() : lu2d_step<NM, K>(acc, rh, pv, __builtin_amdgcn_readlane(pk, K), ln, viol, rpv, sing)), ...);
+                                           bool& bad) {
+  constexpr int NJ = Lu2d<NM>::NJ;
+  const int lc = ln & 15;
+  double piv = bcast(acc[0][0], 0), col[NJ];  // pivot 0 and column 0
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) col[J] = bperm_f64_addr(acc[J][0], lc << 2);
+  (lu2d_step<NM, K>(acc, rh, pv, __builtin_amdgcn_readlane(pk, K), ln, viol, rpv, bad, piv, col), ...);
 }
 
 template <int NM>
@@ -145,9 +166,23 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk
   }
   uint32_t viol = 0;
   double rpv = 0.0;
-  bool sing = false;
-  lu2d_steps<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, pv, pk, ln, viol, rpv, sing);
-  if (sing || ballot(viol != 0)) return false;
+  bool bad = false;
+  lu2d_steps<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, pv, pk, ln, viol, rpv, bad);
+  // a non-finite U entry or reduced rhs: the +0-multiplier updates of the pivot half may
+  // have turned an entry the searched LU keeps into NaN — let the searched LU decide
+  // (checked before U overwrites Srow, so a false return leaves [S | rr] there)
+  bool fin = true;
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) {
+    const int q = lc + 16 * J;
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      const int col = lr + 4 * c;
+      if (q < NM && col < NM && col >= q) fin = fin & __builtin_isfinite(acc[J][c]);
+    }
+    if (q < NM) fin = fin & __builtin_isfinite(rh[J]);
+  }
+  if (bad || ballot((viol != 0) | !fin)) return false;
   __syncthreads();  // every row read before U overwrites Srow
   // U by position (row q of the elimination = the guess's row p_q) and the reduced rhs
 #pragma unroll
@@ -164,12 +199,6 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk
 #pragma unroll
   for (int j = 0; j < NM; ++j) u[j] = Srow[qq * LDR + j];
   double b = Srow[qq * LDR + NM];
-  // a non-finite U entry or rhs: the +0-multiplier updates of the pivot half may have turned
-  // an entry the searched LU keeps into NaN — let the searched LU decide
-  bool fin = __builtin_isfinite(b);
-#pragma unroll
-  for (int j = 0; j < NM; ++j) fin = fin & ((j < ln) | __builtin_isfinite(u[j]));
-  if (ballot(!fin & (ln < NM))) return false;
   double x = 0.0;
 #pragma unroll
   for (int k = NM - 1; k >= 0; --k) {
@@ -179,6 +208,53 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk
   }
   dz = x;  // x_k = δ of column k: lane k holds unknown k
   return true;
+}
+
+// ---- Schur complement into LDS, entry-parallel ---------------------------------------
+// Row i of [S | rr] at Srow[i·LDR], S = (P + tol·I) − Q D⁻¹ R, rr_i = −F_Gi − Σ_k Q_ik ty_k.
+// First P + tol·I and −F_G, one P entry per lane and slot (column-major P: coalesced);
+// then each structural nonzero of Q D⁻¹ R and each rr_i with K(i) ≠ ∅ — an "entry" of the
+// generated tables mcpx_nl_se_pos / mcpx_nl_se_k (codegen.py: slot e = lane + 64r, its
+// position i·LDR + j and its k ascending) — takes its fma chain in one lane:
+// fma(−Q_ik, R_kj·D_k⁻¹, ·) (rr: fma(−Q_ik, ty_k, ·)), k ascending: the oracle's chain
+// for that entry (oracle/ipm_oracle.c, the row-wise loop over K(i) and J(k)).
+template <int LDR>
+__device__ __forceinline__ void schur_form_entries(double* Srow, const double* blk, const double* Fs,
+                                                   const double* sDi, const double* sTy, double tol, int ln) {
+  constexpr int NP = n * n, RP = (NP + 63) / 64;
+#pragma unroll
+  for (int r = 0; r < RP; ++r) {
+    const int t = ln + 64 * r;
+    if (t < NP) {
+      const int j = t / n, i = t - j * n;  // P_ij = blk[OFF_P + j·n + i]
+      const double v = blk[OFF_P + t];
+      Srow[i * LDR + j] = (i == j) ? v + tol : v;
+    }
+  }
+  if (ln < n) Srow[ln * LDR + n] = -Fs[ln];
+  __syncthreads();
+  int pos[MCPX_NL_SE_ER], ks[MCPX_NL_SE_ER][MCPX_NL_SE_KT];
+#pragma unroll
+  for (int r = 0; r < MCPX_NL_SE_ER; ++r) {
+    pos[r] = mcpx_nl_se_pos[64 * r + ln];
+#pragma unroll
+    for (int t = 0; t < MCPX_NL_SE_KT; ++t) ks[r][t] = mcpx_nl_se_k[(r * MCPX_NL_SE_KT + t) * 64 + ln];
+  }
+#pragma unroll
+  for (int r = 0; r < MCPX_NL_SE_ER; ++r) {
+    if (pos[r] < 0) continue;
+    const int i = pos[r] / LDR, j = pos[r] - i * LDR;
+    double v = Srow[pos[r]];
+#pragma unroll
+    for (int t = 0; t < MCPX_NL_SE_KT; ++t) {
+      const int k = ks[r][t];
+      if (k < 0) continue;
+      const double q = -blk[OFF_Q + k * n + i];
+      const double f = (j == n) ? sTy[k] : blk[OFF_R + j * m + k] * sDi[k];
+      v = fma(q, f, v);
+    }
+    Srow[pos[r]] = v;
+  }
 }
 
 // ---- multi-wave LU of the SCHUR kernel (mcpx_nl_solve_schur_mw) ---------------------
@@ -337,6 +413,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   int status = 0;                     // :69
   int outer = 1;                      // :70
   int newton = 0;
+  unsigned reason = 0;  // MCPX_FAIL_* events
   int piv_guess = 0;        // SCHUR: lane k = pivot row of LU step k at the last Newton step
   bool have_guess = false;  // (lu_solve_rows_core)
 #if MCPX_STAMPS
@@ -405,6 +482,31 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
         // lanes ≥ n hold a copy of row 0: never a pivot row, never updated (lu_solve_rows)
         // (MW: wave 0 forms the rows into Srow for lu_solve_mw)
         const int i = lx ? lane : 0;
+        if constexpr (!MW) {
+          schur_form_entries<LDR>(Srow, blk, Fs, sDi, sTy, tol, lane);
+          __syncthreads();
+          MCPX_STAMP(1);
+          // LU of [S | rr] (oracle lu_solve_x, reciprocal multipliers) with the previous
+          // Newton step's pivot sequence as the guess (the lane-change game keeps it on 86 %
+          // of steps): the 2-D elimination (lu2d_solve) reads the rows in the guessed order;
+          // a missed guess leaves Srow as it was and the register LU with the pivot search
+          // factors its rows.  Bits equal the searched LU.  Lanes ≥ n hold a copy of row 0:
+          // never a pivot row, never updated (lu_solve_rows_core).
+          bool miss = true;
+          if (have_guess) {
+            miss = !lu2d_solve<n>(Srow, LDR, lane, piv_guess, dz);
+            ok = !miss;
+          }
+          if (miss) {
+            double a[NMAX];
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j) a[j] = (j < n) ? Srow[i * LDR + j] : 0.0;
+            const double rhs = Srow[i * LDR + n];
+            bool unused;
+            ok = lu_solve_rows_core<NMAX, true>(a, rhs, opaque(n), lane, dz, piv_guess, false, unused);
+          }
+          have_guess = ok;
+        } else {
         if (w0) {
         const double dg = blk[OFF_P + i * n + i] + tol;  // the diagonal entry, one add
         double a[NMAX];
@@ -438,35 +540,10 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
           for (int j = 0; j < n; ++j) a[j] = row[j];
         }
         MCPX_STAMP(1);
-        if constexpr (!MW) {
-        // LU of S (oracle lu_solve_x, reciprocal multipliers) with the previous Newton
-        // step's pivot sequence as the guess (the lane-change game keeps it on 86 % of
-        // steps): the 2-D elimination (lu2d_solve), which reads the rows from Srow in the
-        // guessed order; a missed guess factors the register rows again with the pivot
-        // search.  Bits equal the searched LU.
-        bool miss = true;
-        if (have_guess) {
-          if (lx) {
-            double* row = Srow + i * LDR;
-#pragma unroll
-            for (int j = 0; j < n; ++j) row[j] = a[j];
-            row[n] = rhs;
-          }
-          __syncthreads();
-          miss = !lu2d_solve<n>(Srow, LDR, lane, piv_guess, dz);
-          ok = !miss;
-        }
-        if (miss) {
-          bool unused;
-          ok = lu_solve_rows_core<NMAX, true>(a, rhs, opaque(n), lane, dz, piv_guess, false, unused);
-        }
-        have_guess = ok;
-        }  // !MW
-        }  // w0: S formed (and, one-wave, factored)
-        if constexpr (MW) {
-          __syncthreads();  // every row of [S | rr] in Srow
-          ok = lu_solve_mw<n, 4, NMAX>(Srow, LDR, mwL, mwP, mwPv, wv, lane, dz);
-        }
+        }  // w0: S formed
+        __syncthreads();  // every row of [S | rr] in Srow
+        ok = lu_solve_mw<n, 4, NMAX>(Srow, LDR, mwL, mwP, mwPv, wv, lane, dz);
+        }  // MW
         MCPX_STAMP(2);
         if (ok) {
           if (w0 && lx) dzs[lane] = dz;
@@ -557,6 +634,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
       }
       if (!ok) {  // the failed linear solve of :84-88
         status = 1;
+        reason |= MCPX_FAIL_LINSOLVE;
         break;
       }
       __syncthreads();
@@ -599,6 +677,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
       const int ey = (~vy) ? lowest_lane(~vy) : 64;
       if (es >= args.n_trials || ey >= args.n_trials) {  // α = NaN
         status = 1;
+        reason |= MCPX_FAIL_LINESEARCH;
         break;
       }
       double as = 1.0, ay = 1.0;
@@ -628,7 +707,10 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
     eps *= (status == 0) ? args.tight[inner] : args.loose[inner];  // :111-113
     ++outer;                                                        // :114
   }
-  if (outer == args.max_outer) status = 1;  // :117-119
+  if (outer == args.max_outer) {  // :117-119
+    status = 1;
+    reason |= MCPX_FAIL_MAX_OUTER;
+  }
 
   // ---- outputs (:121) -------------------------------------------------------
   __syncthreads();
@@ -657,6 +739,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
     args.outer_iters[inst] = outer;
     args.status[inst] = status;
     if (args.newton_iters) args.newton_iters[inst] = newton;
+    if (args.fail_reason) args.fail_reason[inst] = (uint8_t)reason;
   }
 }
 
@@ -726,30 +809,30 @@ __device__ int32_t mcpx_nl_meta[12] = {
     MCPX_NL_SIZE, MCPX_NL_NNZ, MCPX_NL_NNZ_T, 0, 0, 0};
 
 #if MCPX_NL_CAN_WG_REDUCED
-__global__ __launch_bounds__(256) void mcpx_nl_vjp_wg(const mcpx::wg::WgSensArgs args) {
+__global__ __launch_bounds__(mcpx::wg::kThreads) void mcpx_nl_vjp_wg(const mcpx::wg::WgSensArgs args) {
   mcpx::wg::sens_instances<MCPX_FAMILY_NONLINEAR, false, mcpx::nl::NVW, MCPX_NL_N + MCPX_NL_M, mcpx::nl::Gen>(args);
 }
 #endif
 #if MCPX_NL_CAN_WG_DENSE
-__global__ __launch_bounds__(256) void mcpx_nl_jvp_wg(const mcpx::wg::WgSensArgs args) {
+__global__ __launch_bounds__(mcpx::wg::kThreads) void mcpx_nl_jvp_wg(const mcpx::wg::WgSensArgs args) {
   mcpx::wg::sens_instances<MCPX_FAMILY_NONLINEAR, true, mcpx::nl::NVW, mcpx::nl::NVW, mcpx::nl::Gen>(args);
 }
 #endif
 
 #if MCPX_NL_CAN_WG_REDUCED
-__global__ __launch_bounds__(256) void mcpx_nl_solve_reduced_wg(const mcpx::wg::WgArgs args) {
+__global__ __launch_bounds__(mcpx::wg::kThreads) void mcpx_nl_solve_reduced_wg(const mcpx::wg::WgArgs args) {
   mcpx::wg::solve_instances<MCPX_FAMILY_NONLINEAR, MCPX_LINSOLVE_REDUCED, mcpx::nl::NVW, MCPX_NL_N + MCPX_NL_M,
                             mcpx::nl::Gen>(args);
 }
 #endif
 #if MCPX_NL_CAN_WG_DENSE
-__global__ __launch_bounds__(256) void mcpx_nl_solve_dense_wg(const mcpx::wg::WgArgs args) {
+__global__ __launch_bounds__(mcpx::wg::kThreads) void mcpx_nl_solve_dense_wg(const mcpx::wg::WgArgs args) {
   mcpx::wg::solve_instances<MCPX_FAMILY_NONLINEAR, MCPX_LINSOLVE_DENSE, mcpx::nl::NVW, mcpx::nl::NVW,
                             mcpx::nl::Gen>(args);
 }
 #endif
 #if MCPX_NL_CAN_WG_SCHUR
-__global__ __launch_bounds__(256) void mcpx_nl_solve_schur_wg(const mcpx::wg::WgArgs args) {
+__global__ __launch_bounds__(mcpx::wg::kThreads) void mcpx_nl_solve_schur_wg(const mcpx::wg::WgArgs args) {
   mcpx::wg::solve_instances<MCPX_FAMILY_NONLINEAR, MCPX_LINSOLVE_SCHUR, mcpx::nl::NVW, MCPX_NL_N, mcpx::nl::Gen>(args);
 }
 #endif

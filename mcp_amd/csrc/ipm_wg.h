@@ -44,7 +44,7 @@ struct WgSensArgs {
   int32_t nrhs;         // right-hand sides per factorisation (JVP partials; 1 for the VJP)
 };
 
-constexpr int kThreads = 256;       // workgroup size of every workgroup kernel
+constexpr int kThreads = 256;       // workgroup size of every workgroup kernel (4 waves)
 constexpr int kMaxDim = 768;        // largest system / vector dimension of the QP / affine kernels
 constexpr int kDimBuckets[4] = {128, 256, 512, 768};
 
@@ -53,8 +53,10 @@ constexpr int kDimBuckets[4] = {128, 256, 512, 768};
 // QP / affine families, MCPX_LINSOLVE_REDUCED or _DENSE, vector dimension
 // n + 2m ≤ nv ∈ wg::kDimBuckets.  The kernel symbol (for the occupancy query)
 // and the launch; hipErrorInvalidValue when no such kernel exists.
-const void* ipm_wg_kernel(int family, int solver, int nv);
-hipError_t launch_ipm_wg(int family, int solver, int nv, const wg::WgArgs& a, int grid, hipStream_t st);
+// ns: rows of the factored system (a system of at most MCPX_VR_MAX rows is factored in
+// registers, lu_vr.hpp).
+const void* ipm_wg_kernel(int family, int solver, int nv, int ns);
+hipError_t launch_ipm_wg(int family, int solver, int nv, int ns, const wg::WgArgs& a, int grid, hipStream_t st);
 // Sensitivity kernels of the QP and affine families beyond the one-wave kernels'
 // 64 rows (sens_inst_wg.hip): VJP (jvp = false) or JVP at vector dimension
 // n + 2m ≤ nv ∈ wg::kDimBuckets.

@@ -35,12 +35,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ipm_wg.h"
 
 namespace mcpx {
 namespace wg {
 
-constexpr int WG = 256;  // threads per workgroup
+constexpr int WG = kThreads;  // threads per workgroup
 constexpr int NWAVE = WG / 64;
 constexpr int NB = 16;   // LU panel width
 
@@ -391,6 +393,14 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
   return true;
 }
 
+}  // namespace wg
+}  // namespace mcpx
+
+#include "lu_vr.hpp"  // the register-resident LU (uses the helpers above)
+
+namespace mcpx {
+namespace wg {
+
 // ---- the solver -------------------------------------------------------------
 
 // The generated code of a nonlinear module (csrc/ipm_nl_kernel.hpp) or nothing.
@@ -485,10 +495,18 @@ __device__ __forceinline__ double jac(const double* __restrict__ th, const doubl
   return 0.0;
 }
 
+// Systems of up to MCPX_VR_MAX rows are factored in registers (lu_vr.hpp), larger ones
+// through the slot's HBM workspace (lu_solve above).
+#ifndef MCPX_VR_MAX
+#define MCPX_VR_MAX 0
+#endif
+template <int NSMAX>
+constexpr bool kVr = NSMAX <= MCPX_VR_MAX;
+
 template <int NVMAX, int NSMAX>
 struct SolveShared {
   double zs[NVMAX], Fs[NVMAX], dzs[NVMAX];
-  LuShared<NSMAX> lu;
+  std::conditional_t<kVr<NSMAX>, VrShared<NSMAX, 1>, LuShared<NSMAX>> lu;
   Scratch sc;
 };
 
@@ -544,6 +562,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
     int status = 0;                     // :69
     int outer = 1;                      // :70
     int newton = 0;
+    unsigned reason = 0;  // MCPX_FAIL_* events
     while (kkt > tol && eps > tol && outer < a.max_outer) {  // :71
       int inner = 1;                                          // :72
       status = 0;                                             // :73
@@ -625,8 +644,12 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
         // ---- LU with partial pivoting (:83-88) ------------------------------------
         // generated nonlinear modules' SCHUR step: reciprocal multipliers (oracle lu_solve_x)
         constexpr bool RCP = FAMILY == MCPX_FAMILY_NONLINEAR && SOLVER == MCPX_LINSOLVE_SCHUR;
-        if (!lu_solve<NSMAX, RCP>(Am, ld, ns, dzs, S.lu)) {
+        bool lu_ok;
+        if constexpr (kVr<NSMAX>) lu_ok = lu_solve_vr<NSMAX, 1, RCP>(Am, ld, ns, dzs, S.lu);
+        else lu_ok = lu_solve<NSMAX, RCP>(Am, ld, ns, dzs, S.lu);
+        if (!lu_ok) {
           status = 1;
+          reason |= MCPX_FAIL_LINSOLVE;
           break;
         }
         if constexpr (SCH) {  // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
@@ -665,6 +688,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
         const int ey = (~vy) ? __ffsll((unsigned long long)~vy) - 1 : 64;
         if (es >= a.n_trials || ey >= a.n_trials) {  // α = NaN
           status = 1;
+          reason |= MCPX_FAIL_LINESEARCH;
           break;
         }
         double as = 1.0, ay = 1.0;
@@ -685,7 +709,10 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
       eps *= (status == 0) ? a.tight[inner] : a.loose[inner];  // :111-113
       ++outer;                                                  // :114
     }
-    if (outer == a.max_outer) status = 1;  // :117-119
+    if (outer == a.max_outer) {  // :117-119
+      status = 1;
+      reason |= MCPX_FAIL_MAX_OUTER;
+    }
     __syncthreads();
 
     // ---- outputs (:121) -------------------------------------------------------------
@@ -707,6 +734,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
       a.outer_iters[inst] = outer;
       a.status[inst] = status;
       if (a.newton_iters) a.newton_iters[inst] = newton;
+      if (a.fail_reason) a.fail_reason[inst] = (uint8_t)reason;
     }
     __syncthreads();
   }

@@ -266,6 +266,7 @@ void set_chunk(mcpx::KernelArgs& a, const mcpx_desc* d, const double* theta, con
   a.active_mask = o->active_mask ? o->active_mask + b0 : nullptr;
   a.alpha_trace = (o->alpha_trace && o->trace_len > 0) ? o->alpha_trace + b0 * (int64_t)o->trace_len * 2 : nullptr;
   a.trace_len = o->alpha_trace ? o->trace_len : 0;
+  a.fail_reason = o->fail_reason ? o->fail_reason + b0 : nullptr;
 }
 
 hipError_t pool_malloc(void** p, size_t bytes, hipStream_t st);  // the library's own pool (below)
@@ -286,7 +287,7 @@ int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const d
     if (rc) return rc;
     HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, mcpx::wg::kThreads, 0));
   } else {
-    kp = mcpx::ipm_wg_kernel(a.family, ls, nv);
+    kp = mcpx::ipm_wg_kernel(a.family, ls, nv, ns);
     if (!kp) return fail(MCPX_EUNSUPPORTED, "no workgroup kernel for family %d, linear_solver %d, dim %d", a.family, ls, nv);
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kp, mcpx::wg::kThreads, 0));
   }
@@ -321,7 +322,7 @@ int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const d
         void* params[] = {&w};
         e = hipModuleLaunchKernel(f, (unsigned)grid, 1, 1, mcpx::wg::kThreads, 1, 1, 0, st, params, nullptr);
       } else {
-        e = mcpx::launch_ipm_wg(a.family, ls, nv, w, grid, st);
+        e = mcpx::launch_ipm_wg(a.family, ls, nv, ns, w, grid, st);
       }
     }
     if (e != hipSuccess) rc = fail(MCPX_EHIP, "workgroup solver launch failed: %s", hipGetErrorString(e));
@@ -525,7 +526,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   AsyncBuf<double> x, y, s, kkt, eps;
   AsyncBuf<int32_t> outer, status, newton;
   AsyncBuf<uint64_t> am;
-  AsyncBuf<uint8_t> tr;
+  AsyncBuf<uint8_t> tr, fr;
   // declared after the buffers, so it runs before their (stream-ordered) frees on every
   // exit: no upload or kernel may still target a buffer when it returns to the pool
   struct Drain {
@@ -547,6 +548,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   HIP_TRY(status.alloc(nb, cs));
   if (o->newton_iters) HIP_TRY(newton.alloc(nb, cs));
   if (o->active_mask) HIP_TRY(am.alloc(nb, cs));
+  if (o->fail_reason) HIP_TRY(fr.alloc(nb, cs));
   const bool want_tr = o->alpha_trace && o->trace_len > 0;
   if (want_tr) {
     HIP_TRY(tr.alloc((size_t)nb * o->trace_len * 2, cs));
@@ -571,6 +573,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
     od.active_mask = am.p ? am.p + c0 : nullptr;
     od.alpha_trace = want_tr ? tr.p + c0 * (int64_t)o->trace_len * 2 : nullptr;
     od.trace_len = want_tr ? o->trace_len : 0;
+    od.fail_reason = fr.p ? fr.p + c0 : nullptr;
     mcpx_desc dd = *d;
     dd.batch = cn;
     if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, cs, mod, wg, mw))) return rc;
@@ -591,6 +594,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   if (o->newton_iters) HIP_TRY(back(o->newton_iters + b0, newton.p, sizeof(int32_t) * nb));
   if (o->active_mask) HIP_TRY(back(o->active_mask + b0, am.p, sizeof(uint64_t) * nb));
   if (want_tr) HIP_TRY(back(o->alpha_trace + b0 * o->trace_len * 2, tr.p, (size_t)nb * o->trace_len * 2));
+  if (o->fail_reason) HIP_TRY(back(o->fail_reason + b0, fr.p, (size_t)nb));
   return MCPX_OK;
 }
 

@@ -64,12 +64,12 @@ def solve_batch(family: int, n: int, m: int, theta: np.ndarray, *, x0=None, y0=N
         x=np.empty((B, n)), y=np.empty((B, m)), s=np.empty((B, m)), kkt_error=np.empty(B),
         eps=np.empty(B), outer_iters=np.empty(B, np.int32), status=np.empty(B, np.int32),
         newton_iters=np.empty(B, np.int32), active_mask=np.empty((B, words), np.uint64),
-        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8), fail_reason=np.empty(B, np.uint8),
     )
     out = Out(_ptr(r["x"]), _ptr(r["y"]), _ptr(r["s"]), _ptr(r["kkt_error"]), _ptr(r["eps"]),
               _ptr(r["outer_iters"]), _ptr(r["status"]), _ptr(r["newton_iters"]),
               _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
-              int(trace_len), 0)
+              int(trace_len), 0, _ptr(r["fail_reason"]))
     desc = Desc(family, n, m, 0, B, ld)
     rc = lib().oracle_solve_batch(C.byref(desc), _ptr(theta), _ptr(x0), _ptr(y0), _ptr(s0),
                                   C.byref(prm), C.byref(out), int(nthreads))
@@ -152,12 +152,12 @@ def solve_batch_nl(nl, theta: np.ndarray, *, x0=None, y0=None, s0=None, params: 
         x=np.empty((B, n)), y=np.empty((B, m)), s=np.empty((B, m)), kkt_error=np.empty(B),
         eps=np.empty(B), outer_iters=np.empty(B, np.int32), status=np.empty(B, np.int32),
         newton_iters=np.empty(B, np.int32), active_mask=np.empty((B, words), np.uint64),
-        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
+        alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8), fail_reason=np.empty(B, np.uint8),
     )
     out = Out(_ptr(r["x"]), _ptr(r["y"]), _ptr(r["s"]), _ptr(r["kkt_error"]), _ptr(r["eps"]),
               _ptr(r["outer_iters"]), _ptr(r["status"]), _ptr(r["newton_iters"]),
               _ptr(r["active_mask"]), _ptr(r["alpha_trace"]) if trace_len > 0 else None,
-              int(trace_len), 0)
+              int(trace_len), 0, _ptr(r["fail_reason"]))
     spec = _nl_spec(nl)
     L = lib()
     L.oracle_solve_batch_nl.restype = C.c_int

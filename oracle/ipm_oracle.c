@@ -359,6 +359,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
   int status = MCPX_STATUS_SOLVED; /* :69 */
   int outer = 1;              /* :70 */
   int newton = 0;
+  unsigned reason = 0;        /* MCPX_FAIL_* events (the `verbose` warnings of :85, :97) */
   int m_sym = 0; /* SCHUR: M exactly symmetric → try the SPD Gauss-Jordan first */
   /* MCPX_FAMILY_NONLINEAR: family_row reads the generated blocks instead of θ */
   const double* fth = th;
@@ -388,6 +389,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
       if (p->linear_solver == MCPX_LINSOLVE_DENSE) {
         if (lu_solve(N, w->J, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
           status = MCPX_STATUS_FAILED;
+          reason |= MCPX_FAIL_LINSOLVE;
           break;
         }
       } else if (p->linear_solver == MCPX_LINSOLVE_SCHUR) {
@@ -459,6 +461,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
         }
         if (!spd_ok && lu_solve_x(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow, nl != NULL)) {
           status = MCPX_STATUS_FAILED;
+          reason |= MCPX_FAIL_LINSOLVE;
           break;
         }
         for (int k = 0; k < m; ++k) {
@@ -491,6 +494,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           for (int j = 0; j < Nr; ++j) w->Jr[(size_t)i * Nr + j] = w->J[(size_t)i * N + j];
         if (lu_solve(Nr, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow)) {
           status = MCPX_STATUS_FAILED;
+          reason |= MCPX_FAIL_LINSOLVE;
           break;
         }
         for (int k = 0; k < m; ++k) {
@@ -504,6 +508,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
       const int ey = linesearch_exponent(z + n, w->dz + n, m, t);
       if (es < 0 || ey < 0) {
         status = MCPX_STATUS_FAILED;
+        reason |= MCPX_FAIL_LINESEARCH;
         break;
       }
       if (o->alpha_trace && newton < o->trace_len) { /* accepted steps only */
@@ -530,7 +535,10 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
     eps *= (status == MCPX_STATUS_SOLVED) ? t->tight[inner] : t->loose[inner]; /* :111-113 */
     ++outer; /* :114 */
   }
-  if (outer == p->max_outer_iters) status = MCPX_STATUS_FAILED; /* :117-119 */
+  if (outer == p->max_outer_iters) { /* :117-119 */
+    status = MCPX_STATUS_FAILED;
+    reason |= MCPX_FAIL_MAX_OUTER;
+  }
   for (int i = 0; i < n; ++i) o->x[inst * n + i] = z[i];
   for (int k = 0; k < m; ++k) o->y[inst * m + k] = z[n + k];
   for (int k = 0; k < m; ++k) o->s[inst * m + k] = z[n + m + k];
@@ -539,6 +547,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
   o->outer_iters[inst] = outer;
   o->status[inst] = status;
   if (o->newton_iters) o->newton_iters[inst] = newton;
+  if (o->fail_reason) o->fail_reason[inst] = (uint8_t)reason;
   if (o->active_mask) {
     const int words = m > 64 ? (m + 63) / 64 : 1;
     uint64_t* am = o->active_mask + (size_t)inst * words;

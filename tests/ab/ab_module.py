@@ -10,7 +10,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
-OUT = os.path.join(ROOT, "tools", "abx")
+OUT = os.environ.get("MCPX_AB_OUT", os.path.join(ROOT, "tools", "abx"))
 
 
 def build(name, csrc, T=2):

@@ -39,6 +39,8 @@ def _rel(a, b):
 def assert_parity(got: dict, ref: dict, bitwise: bool = True):
     for k in INT:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    if got.get("fail_reason") is not None and ref.get("fail_reason") is not None:
+        np.testing.assert_array_equal(np.asarray(got["fail_reason"]), ref["fail_reason"], err_msg="fail_reason")
     np.testing.assert_array_equal(got["active_mask"], ref["active_mask"], err_msg="active_mask")
     if "alpha_trace" in ref and ref["alpha_trace"].size and got["alpha_trace"].size:
         L = min(got["alpha_trace"].shape[1], ref["alpha_trace"].shape[1])

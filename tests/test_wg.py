@@ -25,6 +25,8 @@ TRACE = 1024
 def assert_bit_exact(got, ref):
     for k in INT:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    if got.get("fail_reason") is not None and ref.get("fail_reason") is not None:
+        np.testing.assert_array_equal(np.asarray(got["fail_reason"]), ref["fail_reason"], err_msg="fail_reason")
     if got.get("active_mask") is not None:
         np.testing.assert_array_equal(got["active_mask"], ref["active_mask"], err_msg="active_mask")
     if got.get("alpha_trace") is not None and got["alpha_trace"].size:
