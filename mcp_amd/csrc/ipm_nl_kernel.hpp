@@ -782,6 +782,9 @@ struct Gen {
   __device__ static const int32_t* qk_idx() { return mcpx_nl_qk_idx; }
   __device__ static const int32_t* rj_ptr() { return mcpx_nl_rj_ptr; }
   __device__ static const int32_t* rj_idx() { return mcpx_nl_rj_idx; }
+  static constexpr int SE_ER = MCPX_NL_SE_ER, SE_KT = MCPX_NL_SE_KT;
+  __device__ static const int32_t* se_pos() { return mcpx_nl_se_pos; }
+  __device__ static const int32_t* se_k() { return mcpx_nl_se_k; }
   __device__ static void eval_theta(const double* th, const double* z, double* dth) { mcpx_nl_eval_theta(th, z, dth); }
   __device__ static const int32_t* tc_ptr() { return mcpx_nl_tc_ptr; }
   __device__ static const int32_t* tc_idx() { return mcpx_nl_tc_idx; }

@@ -418,6 +418,9 @@ struct NoGen {
   __device__ static const int32_t* qk_idx() { return nullptr; }
   __device__ static const int32_t* rj_ptr() { return nullptr; }
   __device__ static const int32_t* rj_idx() { return nullptr; }
+  static constexpr int SE_ER = 1, SE_KT = 1;
+  __device__ static const int32_t* se_pos() { return nullptr; }
+  __device__ static const int32_t* se_k() { return nullptr; }
 };
 
 // Row i of F (src/mcp.jl:76-80) at z = zs, oracle family_row() op for op.
@@ -498,15 +501,33 @@ __device__ __forceinline__ double jac(const double* __restrict__ th, const doubl
 // Systems of up to MCPX_VR_MAX rows are factored in registers (lu_vr.hpp), larger ones
 // through the slot's HBM workspace (lu_solve above).
 #ifndef MCPX_VR_MAX
-#define MCPX_VR_MAX 0
+#define MCPX_VR_MAX 200
 #endif
 template <int NSMAX>
 constexpr bool kVr = NSMAX <= MCPX_VR_MAX;
 
-template <int NVMAX, int NSMAX>
+// lu_solve_vr's patch of the nonlinear SCHUR step: the entries of column tile tc among the
+// generated mcpx_nl_se_* entries (position i·(n+1) + j, value sv[e]).
+template <class GEN>
+struct SePatch {
+  static constexpr bool active = true;
+  const double* sv;
+  int n;
+  __device__ void operator()(int tc, double* pan, int PL) const {
+    const int32_t* sp = GEN::se_pos();
+    for (int e = threadIdx.x; e < 64 * GEN::SE_ER; e += WG) {
+      const int pos = sp[e];
+      if (pos < 0) continue;
+      const int i = pos / (n + 1), j = pos - i * (n + 1);
+      if ((j >> 4) == tc) pan[i * PL + (j & 15)] = sv[e];
+    }
+  }
+};
+
+template <int NVMAX, int NSMAX, bool VR = kVr<NSMAX>>
 struct SolveShared {
   double zs[NVMAX], Fs[NVMAX], dzs[NVMAX];
-  std::conditional_t<kVr<NSMAX>, VrShared<NSMAX, 1>, LuShared<NSMAX>> lu;
+  std::conditional_t<VR, VrShared<NSMAX, 1>, LuShared<NSMAX>> lu;
   Scratch sc;
 };
 
@@ -525,7 +546,6 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
   double* const slot = W.work + (int64_t)blockIdx.x * W.slot_stride;
   double* const Am = slot;
   double* const blk = slot + W.off_blk;
-  double* const RD = slot + W.off_rd;
   double* const sD = slot + W.off_aux;
   double* const srw = sD + m;
   double* const sry = sD + 2 * m;
@@ -533,6 +553,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
   double* const zs = S.zs;
   double* const Fs = S.Fs;
   double* const dzs = S.dzs;
+  __shared__ double sv[SCH && kVr<NSMAX> ? 64 * GEN::SE_ER : 1];  // VR SCHUR: the sparse entries of [S | rr]
 
   for (;;) {
     if (tid == 0) S.sc.inst = atomicAdd(W.counter, 1);  // the work queue
@@ -593,39 +614,62 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
             sty[k] = ry * Di;
           }
           __syncthreads();
-          for (int k = wave; k < m; k += NWAVE)  // R_kj · D_k⁻¹, row k (wave per row, lanes over j)
-            for (int j = lane; j < n; j += 64) RD[k * n + j] = blk[GEN::OFF_R + j * m + k] * sD[k];
+        }
+        // VR SCHUR: the entries of [S | rr] beyond P + tol·I and −F_G (the generated
+        // mcpx_nl_se_* tables: 360 at T = 10), each with its fma chain, once per step into
+        // LDS; the LU's staging writes them over the dense part (`patch`)
+        if constexpr (SCH && kVr<NSMAX>) {
+          const int32_t* sp = GEN::se_pos();
+          const int32_t* sk = GEN::se_k();
+          for (int e = tid; e < 64 * GEN::SE_ER; e += WG) {
+            const int pos = sp[e];
+            if (pos < 0) continue;
+            const int i = pos / (n + 1), j = pos - i * (n + 1), r = e >> 6, l = e & 63;
+            double v = j < n ? blk[GEN::OFF_P + j * n + i] : -Fs[i];
+            if (i == j) v += tol;
+#pragma unroll
+            for (int t = 0; t < GEN::SE_KT; ++t) {
+              const int k = sk[(r * GEN::SE_KT + t) * 64 + l];
+              if (k < 0) continue;
+              v = fma(-blk[GEN::OFF_Q + k * n + i], j < n ? blk[GEN::OFF_R + j * m + k] * sD[k] : sty[k], v);
+            }
+            sv[e] = v;
+          }
           __syncthreads();
-          // S = (P + tol·I) + Σ (−Q_ik)(R_kj D_k⁻¹) over k ∈ K(i) (Q's structural nonzeros of
-          // row i) with j ∈ J(k) (R's of row k), k ascending (the oracle's terms), and
-          // rr_i = −F_Gi + Σ_{k ∈ K(i)} (−Q_ik) ty_k
-          const int32_t* qp = GEN::qk_ptr();
-          const int32_t* qi = GEN::qk_idx();
-          const int32_t* rp = GEN::rj_ptr();
-          const int32_t* ri = GEN::rj_idx();
-          for (int i = wave; i < n; i += NWAVE)
-            for (int j = lane; j < n; j += 64) {  // wave per row i, lanes over j
-            double acc = blk[GEN::OFF_P + j * n + i];
-            if (i == j) acc += tol;
-            for (int t = qp[i]; t < qp[i + 1]; ++t) {
-              const int k = qi[t];
-              bool nz = false;
-              for (int u = rp[k]; u < rp[k + 1]; ++u) nz |= ri[u] == j;
-              if (nz) acc = fma(-blk[GEN::OFF_Q + k * n + i], RD[k * n + j], acc);
+        }
+        // ---- entry (i, j) of [K | rhs] ------------------------------------------------
+        // SCHUR: S = (P + tol·I) + Σ (−Q_ik)(R_kj·D_k⁻¹) over k ∈ K(i) (Q's structural
+        // nonzeros of row i) with j ∈ J(k) (R's of row k), k ascending (the oracle's terms),
+        // and rr_i = −F_Gi + Σ_{k ∈ K(i)} (−Q_ik) ty_k; otherwise ∇F_z + tol·I (RED: with
+        // the slack block eliminated) and −F.
+        auto entry = [&](int i, int j) -> double {
+          if constexpr (SCH && kVr<NSMAX>) {  // the dense part; sv patches the rest
+            if (j < n) return i == j ? blk[GEN::OFF_P + j * n + i] + tol : blk[GEN::OFF_P + j * n + i];
+            return -Fs[i];
+          } else if constexpr (SCH) {
+            const int32_t* qp = GEN::qk_ptr();
+            const int32_t* qi = GEN::qk_idx();
+            const int32_t* rp = GEN::rj_ptr();
+            const int32_t* ri = GEN::rj_idx();
+            double acc;
+            if (j < n) {
+              acc = blk[GEN::OFF_P + j * n + i];
+              if (i == j) acc += tol;
+              for (int t = qp[i]; t < qp[i + 1]; ++t) {
+                const int k = qi[t];
+                bool nz = false;
+                for (int u = rp[k]; u < rp[k + 1]; ++u) nz |= ri[u] == j;
+                if (nz) acc = fma(-blk[GEN::OFF_Q + k * n + i], blk[GEN::OFF_R + j * m + k] * sD[k], acc);
+              }
+            } else {
+              acc = -Fs[i];
+              for (int t = qp[i]; t < qp[i + 1]; ++t) {
+                const int k = qi[t];
+                acc = fma(-blk[GEN::OFF_Q + k * n + i], sty[k], acc);
+              }
             }
-            Am[(int64_t)i * ld + j] = acc;
-          }
-          for (int i = tid; i < n; i += WG) {
-            double acc = -Fs[i];
-            for (int t = qp[i]; t < qp[i + 1]; ++t) {
-              const int k = qi[t];
-              acc = fma(-blk[GEN::OFF_Q + k * n + i], sty[k], acc);
-            }
-            Am[(int64_t)i * ld + n] = acc;
-          }
-        } else {
-          for (int i = wave; i < ns; i += NWAVE)
-            for (int j = lane; j <= ns; j += 64) {  // wave per row i, lanes over the ns + 1 columns
+            return acc;
+          } else {
             double v;
             if (j < ns) {
               v = jac<FAMILY, GEN>(th, blk, zs, n, m, i, j);
@@ -637,16 +681,23 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
               v = -Fs[i];
               if (RED && i >= n) v = v - (Fs[i + m] / (zs[i] + tol));  // −F_H − F_C / w_k
             }
-            Am[(int64_t)i * ld + j] = v;
+            return v;
           }
-        }
-        __syncthreads();
+        };
         // ---- LU with partial pivoting (:83-88) ------------------------------------
         // generated nonlinear modules' SCHUR step: reciprocal multipliers (oracle lu_solve_x)
         constexpr bool RCP = FAMILY == MCPX_FAMILY_NONLINEAR && SOLVER == MCPX_LINSOLVE_SCHUR;
         bool lu_ok;
-        if constexpr (kVr<NSMAX>) lu_ok = lu_solve_vr<NSMAX, 1, RCP>(Am, ld, ns, dzs, S.lu);
-        else lu_ok = lu_solve<NSMAX, RCP>(Am, ld, ns, dzs, S.lu);
+        if constexpr (kVr<NSMAX> && SCH) {  // entries straight into registers (lu_vr.hpp)
+          lu_ok = lu_solve_vr<NSMAX, 1, RCP>(entry, ns, dzs, S.lu, 1, nullptr, SePatch<GEN>{sv, n});
+        } else if constexpr (kVr<NSMAX>) {
+          lu_ok = lu_solve_vr<NSMAX, 1, RCP>(entry, ns, dzs, S.lu);
+        } else {  // [K | rhs] into the slot's workspace, then the HBM LU
+          for (int i = wave; i < ns; i += NWAVE)
+            for (int j = lane; j <= ns; j += 64) Am[(int64_t)i * ld + j] = entry(i, j);  // wave per row
+          __syncthreads();
+          lu_ok = lu_solve<NSMAX, RCP>(Am, ld, ns, dzs, S.lu);
+        }
         if (!lu_ok) {
           status = 1;
           reason |= MCPX_FAIL_LINSOLVE;

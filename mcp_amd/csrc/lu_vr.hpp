@@ -8,15 +8,15 @@
 //
 // The difference is where [K | rhs] lives while it is factored: wg::lu_solve streams
 // it through the slot's HBM workspace at every panel (the trailing update reads and
-// writes the whole trailing matrix once per 16 columns), while here it is read once
-// into the VGPRs of the workgroup's WG threads in the MFMA accumulator layout and never
-// written back.  Tile (ti, tj) of 16×16 (rows 16ti.., columns 16tj.., right-hand sides
+// writes the whole trailing matrix once per 16 columns), while here its entries are
+// computed straight into the VGPRs of the workgroup's WG threads, in the MFMA
+// accumulator layout, and the matrix never touches memory.  Tile (ti, tj) of 16×16 (rows 16ti.., columns 16tj.., right-hand sides
 // as trailing columns) belongs to wave t mod NWAVE with t = tj·R + ti (column-major:
 // every column tile spreads over the waves, so each panel's trailing update is
 // balanced); in it lane (lr, lc) holds rows 16ti + lr + 4e (e < 4) of column 16tj + lc,
 // the f64 MFMA's C layout.  Only the panel (all rows × 16 columns), the panel's U12 rows
-// and the per-row bookkeeping pass through LDS.  At NSMAX = 208, 8 waves: 23 tiles = 92
-// doubles per lane.
+// and the per-row bookkeeping pass through LDS.  At NSMAX = 200 on 4 waves: 44 tiles = 176
+// doubles per lane (VGPRs and AGPRs; one workgroup per CU).
 #pragma once
 
 namespace mcpx {
@@ -57,26 +57,32 @@ struct VrShared {
   int8_t ps[NSMAX];        // the row's step within the current panel, −1 otherwise
 };
 
-// Pivot of panel column kk among the remaining rows (thread = row), one barrier.
+// Wave-wide max of an unsigned 32-bit key (DPP row_shr 1/2/4/8, row_bcast 15/31), uniform.
+__device__ __forceinline__ uint32_t vr_wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Pivot among the remaining rows (thread = row; key 0 = not a candidate, pivot_key
+// otherwise): the largest key, ties to the smallest row.  Each wave reduces by DPP (the
+// 64-bit key as two 32-bit maxima, then the lowest lane holding it: rows ascend with the
+// lane), then the wave results meet in LDS (double-buffered by step parity): one barrier.
 template <int NSMAX, int NRHS>
-__device__ __forceinline__ int vr_pivot(VrShared<NSMAX, NRHS>& L, int ns, int kk, int step) {
-  constexpr int PL = VrDims<NSMAX, NRHS>::PL;
-  const int tid = threadIdx.x, wave = tid >> 6;
-  uint64_t key = 0;
-  int pos = -1;
-  if (tid < ns && L.step_of[tid] < 0) {
-    key = pivot_key(L.pan[tid * PL + kk]);
-    pos = tid;
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const uint64_t k2 = shfl_xor_u64(key, o);
-    const int p2 = __shfl_xor(pos, o);
-    better(key, pos, k2, p2);
-  }
-  if ((tid & 63) == 0) {
-    L.key[step & 1][wave] = key;
-    L.kpos[step & 1][wave] = pos;
+__device__ __forceinline__ int vr_pivot(VrShared<NSMAX, NRHS>& L, uint64_t key, int step) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t khi = (uint32_t)(key >> 32), klo = (uint32_t)key;
+  const uint32_t mhi = vr_wave_max_u32(khi);
+  const uint32_t mlo = vr_wave_max_u32(khi == mhi ? klo : 0u);
+  const uint64_t win = __ballot(khi == mhi && klo == mlo);
+  if (lane == 0) {
+    const uint64_t wk = ((uint64_t)mhi << 32) | mlo;
+    L.key[step & 1][wave] = wk;
+    L.kpos[step & 1][wave] = wk ? (wave << 6) + (int)__ffsll((unsigned long long)win) - 1 : -1;
   }
   __syncthreads();
   uint64_t k = L.key[step & 1][0];
@@ -86,32 +92,60 @@ __device__ __forceinline__ int vr_pivot(VrShared<NSMAX, NRHS>& L, int ns, int kk
   return p;
 }
 
-// A: ns × (ns + nrhs) row-major (stride ld), read once, not modified.  x (LDS, ≥ ns):
-// the solution of the last right-hand side; with xout also every right-hand side's at
-// xout[c·ns + k].  false: an exact zero pivot (the failed solve of src/solver.jl:84-88).
-template <int NSMAX, int NRHS, bool RCP>
-__device__ __forceinline__ bool lu_solve_vr(const double* __restrict__ A, int ld, int ns, double* x,
-                                            VrShared<NSMAX, NRHS>& L, int nrhs = 1,
-                                            double* __restrict__ xout = nullptr) {
+// entry(i, j): entry (i, j) of [K | rhs] (i < ns, j < ns + nrhs), computed once each, one
+// column tile at a time into LDS and from there into the owners' tiles — the matrix is
+// never written to memory.  x (LDS, ≥ ns): the solution of the last right-hand side; with
+// xout also every right-hand side's at xout[c·ns + k].  false: an exact zero pivot (the
+// failed solve of src/solver.jl:84-88).
+struct NoPatch {
+  static constexpr bool active = false;
+  __device__ void operator()(int, double*, int) const {}
+};
+
+// `patch(tc, pan, PL)` (when active): every thread writes entries of column tile tc that
+// differ from `entry` into the staged tile (pan[i·PL + j − 16·tc]) — the nonlinear SCHUR
+// step's sparse Q D⁻¹ R terms, computed once per step beside the dense P + tol·I.
+template <int NSMAX, int NRHS, bool RCP, class Entry, class Patch = NoPatch>
+__device__ __forceinline__ bool lu_solve_vr(const Entry& entry, int ns, double* x, VrShared<NSMAX, NRHS>& L,
+                                            int nrhs = 1, double* __restrict__ xout = nullptr,
+                                            const Patch& patch = Patch{}) {
   using D = VrDims<NSMAX, NRHS>;
-  constexpr int R = D::R, TPW = D::TPW, PL = D::PL, UL = D::UL;
+  constexpr int R = D::R, T = D::T, TPW = D::TPW, PL = D::PL, UL = D::UL;
   static_assert(NSMAX <= WG, "one thread per row");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lr = lane >> 4, lc = lane & 15;
   const int ncols = ns + nrhs;
   d4 acc[TPW];
-  // ---- [K | rhs] into the tiles (the only read of A) -------------------------------
-#pragma unroll
-  for (int u = 0; u < TPW; ++u) {
-    const int t = vr_opaque(wave) + NWAVE * u, ti = t % R, tj = t / R;
-      const int ln_ = vr_opaque_lane(lane), lr = ln_ >> 4, lc = ln_ & 15;
-    const int col = 16 * tj + lc;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = 16 * ti + lr + 4 * e;
-      acc[u][e] = (row < ns && col < ncols) ? A[(int64_t)row * ld + col] : 0.0;
+  // ---- [K | rhs] into the tiles, one column tile at a time through the panel buffer --
+  for (int tc = 0; tc < T; ++tc) {
+    if (16 * tc >= ncols) break;  // uniform
+    for (int q = tid; q < ns * 16; q += WG) {  // column-major: consecutive threads, consecutive rows
+      const int c = q / ns, i = q - c * ns, j = 16 * tc + c;
+      L.pan[i * PL + c] = j < ncols ? entry(i, j) : 0.0;
     }
+    __syncthreads();
+    if constexpr (Patch::active) {
+      patch(tc, L.pan, PL);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+      __builtin_amdgcn_sched_barrier(0);
+      const int t = vr_opaque(wave) + NWAVE * u, ti = t % R, tj = t / R;
+      const int ln_ = vr_opaque_lane(lane), lr = ln_ >> 4, lc = ln_ & 15;
+      if (tj != tc) continue;  // uniform
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 16 * ti + lr + 4 * e;
+        acc[u][e] = row < ns ? L.pan[row * PL + lc] : 0.0;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < TPW; ++u) {  // tiles beyond the last column: zero
+    const int t = vr_opaque(wave) + NWAVE * u, tj = t / R;
+    if (16 * tj >= ncols) acc[u] = d4{0.0, 0.0, 0.0, 0.0};
   }
   if (tid < NSMAX) L.step_of[tid] = -1;
   int step = 0;
@@ -131,21 +165,41 @@ __device__ __forceinline__ bool lu_solve_vr(const double* __restrict__ A, int ld
       }
     }
     if (tid < NSMAX) L.ps[tid] = -1;
-    // ---- factor it column by column (thread = row; one barrier per column) ---------
-    for (int kk = 0; kk < kb; ++kk, ++step) {
-      const int pp = vr_pivot(L, ns, kk, step);  // barrier inside: the previous update is visible
-      const double piv = L.pan[pp * PL + kk];
-      if (piv == 0.0) return false;
-      const double rp = RCP ? 1.0 / piv : 1.0;
-      if (tid == pp) {
-        L.step_of[pp] = (int16_t)(k0 + kk);
-        L.prow[k0 + kk] = (int16_t)pp;
-        L.ps[pp] = (int8_t)kk;
-      } else if (tid < ns && L.step_of[tid] < 0) {
-        double* row = L.pan + tid * PL;
-        const double l = RCP ? row[kk] * rp : row[kk] / piv;
-        for (int jj = kk + 1; jj < kb; ++jj) row[jj] = fma(-l, L.pan[pp * PL + jj], row[jj]);
-        row[kk] = l;  // a_ik of a remaining row is never read again: keep l_ik there
+    __syncthreads();  // the staged panel before the first pivot search reads other tiles' rows
+    // ---- factor it column by column: thread = row, its panel row in registers; after
+    //      each column a remaining row stores its updated entries back, so the next
+    //      pivot row is in LDS for everyone (one barrier per column) --------------------
+    {
+      double pr[16];
+      const bool own = tid < ns;
+      bool rem = own && L.step_of[own ? tid : 0] < 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) pr[q] = (own && q < kb) ? L.pan[tid * PL + q] : 0.0;
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        if (kk >= kb) continue;  // uniform
+        const int pp = vr_pivot(L, rem ? pivot_key(pr[kk]) : 0ull, step);  // barrier inside
+        ++step;
+        const double* prw = L.pan + pp * PL;
+        const double piv = prw[kk];
+        if (piv == 0.0) return false;  // the failed linear solve of src/solver.jl:84-88
+        if (tid == pp) {
+          rem = false;
+          L.step_of[pp] = (int16_t)(k0 + kk);
+          L.prow[k0 + kk] = (int16_t)pp;
+          L.ps[pp] = (int8_t)kk;
+        } else if (rem) {
+          const double l = RCP ? pr[kk] * (1.0 / piv) : pr[kk] / piv;
+          double* row = L.pan + tid * PL;
+#pragma unroll
+          for (int jj = kk + 1; jj < 16; ++jj) {
+            if (jj >= kb) continue;
+            pr[jj] = fma(-l, prw[jj], pr[jj]);
+            row[jj] = pr[jj];
+          }
+          pr[kk] = l;  // a_ik of a remaining row is never read again: keep l_ik there
+          row[kk] = l;
+        }
       }
     }
     __syncthreads();
@@ -169,9 +223,12 @@ __device__ __forceinline__ bool lu_solve_vr(const double* __restrict__ A, int ld
     __syncthreads();
     // ---- U12: in-panel forward substitution (thread = trailing column) -------------
     for (int j = j_lo + tid; j < ncols; j += WG) {  // (u_k2j re-read from LDS: the tiles hold the registers)
-      for (int kk = 1; kk < kb; ++kk) {
+#pragma unroll
+      for (int kk = 1; kk < 16; ++kk) {
+        if (kk >= kb) continue;  // uniform
         const double* lrow = L.pan + L.prow[k0 + kk] * PL;
         double v = L.u12[kk * UL + j];
+#pragma unroll
         for (int k2 = 0; k2 < kk; ++k2) v = fma(-lrow[k2], L.u12[k2 * UL + j], v);
         L.u12[kk * UL + j] = v;
       }
@@ -250,10 +307,13 @@ __device__ __forceinline__ bool lu_solve_vr(const double* __restrict__ A, int ld
         const int p = L.prow[k0 + j];
         const double* up = L.pan + p * PL;
         double bj = L.bv[p];
-        for (int q = kb - 1; q >= 0; --q) {
+#pragma unroll
+        for (int q = 15; q >= 0; --q) {
+          if (q >= kb) continue;  // uniform
           const double uq = up[q];
           const double tq = RCP ? bj * (1.0 / uq) : bj / uq;  // lane q: x_{k0+q} = b_p / u_pk
-          const double xq = __shfl(tq, q);
+          const double xq = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(tq), q),
+                                             __builtin_amdgcn_readlane(__double2loint(tq), q));
           if (lane == q) x[k0 + q] = xq;
           if (lane < q) bj = fma(-uq, xq, bj);
         }

@@ -120,7 +120,7 @@ __device__ __forceinline__ double dtheta_entry(int64_t t, const double* lam, con
 template <int FAMILY, bool JVP, int NVMAX, int NSMAX, class GEN>
 __device__ __forceinline__ void sens_instances(const WgSensArgs& W) {
   constexpr bool NL = FAMILY == MCPX_FAMILY_NONLINEAR;
-  __shared__ SolveShared<NVMAX, NSMAX> S;
+  __shared__ SolveShared<NVMAX, NSMAX, false> S;  // several right-hand sides: the HBM LU
   const SensArgs& a = W.s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = a.n, m = a.m, N = n + 2 * m, nr = n + m;

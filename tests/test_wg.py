@@ -106,8 +106,9 @@ def test_forced_workgroup_equals_oracle_small(gpu, oracle_lib, n, m, sp, B, seed
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,ls,B", [(64, 32, "dense", 16), (64, 32, "reduced", 16), (128, 64, "dense", 6),
-                                      (100, 78, "reduced", 6), (300, 200, "dense", 2)],
-                         ids=["N128-dense", "N128-reduced", "N256-dense", "N256-reduced", "N700-dense"])
+                                      (100, 78, "reduced", 6), (128, 64, "reduced", 6), (300, 200, "dense", 2)],
+                         ids=["N128-dense", "N128-reduced", "N256-dense", "N256-reduced", "N256-reduced192",
+                              "N700-dense"])
 def test_large_qp_vs_oracle(gpu, oracle_lib, n, m, ls, B):
     """Dense random QPs beyond one wave (N = n + 2m = 128, 256, 700): the blocked LU
     with MFMA trailing updates against the oracle's unblocked LU, bit for bit."""

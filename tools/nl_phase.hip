@@ -13,6 +13,7 @@ int main(int argc, char** argv) {
   const char *mod = argv[1], *kname = argv[2], *thf = argv[3];
   const int n = atoi(argv[4]), m = atoi(argv[5]), p = atoi(argv[6]), B = atoi(argv[7]);
   const unsigned threads = argc > 8 ? (unsigned)atoi(argv[8]) : 64u;
+  const int NST = argc > 9 ? atoi(argv[9]) : 4;  // stamps per instance (5: the LU elimination split out)
   std::vector<double> th((size_t)B * p);
   FILE* f = fopen(thf, "rb");
   if (!f || fread(th.data(), 8, th.size(), f) != th.size()) { fprintf(stderr, "theta read failed\n"); return 2; }
@@ -31,7 +32,7 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&x, (size_t)B * n * 8); (void)hipMalloc(&y, (size_t)B * m * 8); (void)hipMalloc(&s, (size_t)B * m * 8);
   (void)hipMalloc(&kkt, B * 8); (void)hipMalloc(&eps, B * 8);
   (void)hipMalloc(&outer, B * 4); (void)hipMalloc(&status, B * 4); (void)hipMalloc(&newton, B * 4);
-  (void)hipMalloc(&stamps, (size_t)B * 4 * 8);
+  (void)hipMalloc(&stamps, (size_t)B * NST * 8);
   mcpx::KernelArgs a{};
   a.theta = dth; a.theta_ld = p; a.x = x; a.y = y; a.s = s; a.kkt_error = kkt; a.eps = eps;
   a.outer_iters = outer; a.status = status; a.newton_iters = newton; a.stamps = stamps;
@@ -50,23 +51,23 @@ int main(int argc, char** argv) {
     (void)hipDeviceSynchronize();
     (void)hipEventElapsedTime(&ms, e0, e1);
   }
-  std::vector<uint64_t> st((size_t)B * 4);
+  std::vector<uint64_t> st((size_t)B * NST);
   std::vector<int> nw(B), stt(B);
   (void)hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost);
   (void)hipMemcpy(nw.data(), newton, B * 4, hipMemcpyDeviceToHost);
   (void)hipMemcpy(stt.data(), status, B * 4, hipMemcpyDeviceToHost);
-  const char* nm[] = {"eval+F+kkt", "schur prep+form", "LU", "dy/ds+linesearch+update"};
+  const char* nm[] = {"eval+F+kkt", "schur prep+form", "LU (rest)", "dy/ds+linesearch+update", "LU elimination (2-D)"};
   for (int grp = 0; grp < 2; ++grp) {  // solved, failed
-    double tot[4] = {0, 0, 0, 0}, steps = 0; int cnt = 0, mx = 0;
+    double tot[5] = {0, 0, 0, 0, 0}, steps = 0; int cnt = 0, mx = 0;
     for (int b = 0; b < B; ++b) {
       if ((stt[b] != 0) != (grp == 1)) continue;
-      for (int i = 0; i < 4; ++i) tot[i] += st[(size_t)b * 4 + i];
+      for (int i = 0; i < NST; ++i) tot[i] += st[(size_t)b * NST + i];
       steps += nw[b]; ++cnt; mx = nw[b] > mx ? nw[b] : mx;
     }
-    const double all = tot[0] + tot[1] + tot[2] + tot[3];
+    const double all = tot[0] + tot[1] + tot[2] + tot[3] + tot[4];
     printf("[%s] B=%d kernel %.3f ms  %s: %d instances, newton mean %.1f max %d, cycles per Newton step %.0f\n", kname,
            B, ms, grp ? "failed" : "solved", cnt, cnt ? steps / cnt : 0.0, mx, steps ? all / steps : 0.0);
-    for (int i = 0; i < 4; ++i) printf("  %-26s %5.1f%%  %8.0f cyc/step\n", nm[i], all ? 100 * tot[i] / all : 0.0, steps ? tot[i] / steps : 0.0);
+    for (int i = 0; i < NST; ++i) printf("  %-26s %5.1f%%  %8.0f cyc/step\n", nm[i], all ? 100 * tot[i] / all : 0.0, steps ? tot[i] / steps : 0.0);
   }
   return 0;
 }
