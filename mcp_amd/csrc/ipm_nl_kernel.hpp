@@ -148,6 +148,51 @@ __device__ __forceinline__ void lu2d_steps(std::integer_sequence<int, K...>,
   (lu2d_step<NM, K>(acc, rh, pv, __builtin_amdgcn_readlane(pk, K), ln, viol, rpv, bad, piv, col), ...);
 }
 
+// Column k of U for every lane's positions (lanes (·, lc) get position lc + 16J from DPP row
+// Qk), J ≤ Jk only.
+template <int NM, int K>
+__device__ __forceinline__ void lu2d_ucol(const double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], int ln,
+                                          double (&uc)[Lu2d<NM>::NJ]) {
+  constexpr int NJ = Lu2d<NM>::NJ, Jk = K >> 4, Qk = K & 3, Ck = K >> 2;
+  const int addr = (16 * Qk + (ln & 15)) << 2;
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) uc[J] = J <= Jk ? bperm_f64_addr(acc[J][Ck], addr) : 0.0;
+}
+
+template <int NM, int K>
+__device__ __forceinline__ void lu2d_backsub_step(const double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB],
+                                                  double (&rh)[Lu2d<NM>::NJ], double rpv, int ln, double& x,
+                                                  double (&u0)[Lu2d<NM>::NJ], double (&u1)[Lu2d<NM>::NJ],
+                                                  double (&u2)[Lu2d<NM>::NJ]) {
+  constexpr int NJ = Lu2d<NM>::NJ, Jk = K >> 4, Rk = K & 15;
+  __builtin_amdgcn_sched_barrier(0);
+  // u0 = column K (fetched two steps ago); start the fetch of column K − 3 into a free slot
+  double nx[NJ];
+  if constexpr (K >= 3) lu2d_ucol<NM, K - 3>(acc, ln, nx);
+  const double xk = bcast(rh[Jk], Rk) * bcast(rpv, K);  // position K's x (every DPP row holds rh)
+  if (ln == K) x = xk;
+#pragma unroll
+  for (int J = 0; J <= Jk; ++J) rh[J] = fma(-u0[J], xk, rh[J]);
+#pragma unroll
+  for (int J = 0; J < NJ; ++J) {
+    u0[J] = u1[J];
+    u1[J] = u2[J];
+    if constexpr (K >= 3) u2[J] = nx[J];
+  }
+}
+
+template <int NM, int... I>
+__device__ __forceinline__ void lu2d_backsub(std::integer_sequence<int, I...>,
+                                             const double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB],
+                                             double (&rh)[Lu2d<NM>::NJ], double rpv, int ln, double& x) {
+  constexpr int NJ = Lu2d<NM>::NJ;
+  double u0[NJ], u1[NJ], u2[NJ];
+  lu2d_ucol<NM, NM - 1>(acc, ln, u0);
+  if constexpr (NM >= 2) lu2d_ucol<NM, NM - 2>(acc, ln, u1);
+  if constexpr (NM >= 3) lu2d_ucol<NM, NM - 3>(acc, ln, u2);
+  (lu2d_backsub_step<NM, NM - 1 - I>(acc, rh, rpv, ln, x, u0, u1, u2), ...);
+}
+
 template <int NM>
 __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk, double& dz) {
   constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
@@ -183,29 +228,14 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk
     if (q < NM) fin = fin & __builtin_isfinite(rh[J]);
   }
   if (bad || ballot((viol != 0) | !fin)) return false;
-  __syncthreads();  // every row read before U overwrites Srow
-  // U by position (row q of the elimination = the guess's row p_q) and the reduced rhs
-#pragma unroll
-  for (int J = 0; J < NJ; ++J) {
-    const int q = lc + 16 * J;
-#pragma unroll
-    for (int c = 0; c < NCB; ++c)
-      if (q < NM && lr + 4 * c < NM) Srow[q * LDR + lr + 4 * c] = acc[J][c];
-    if (q < NM && lr == 0) Srow[q * LDR + NM] = rh[J];
-  }
-  __syncthreads();
-  double u[NM];
-  const int qq = ln < NM ? ln : 0;
-#pragma unroll
-  for (int j = 0; j < NM; ++j) u[j] = Srow[qq * LDR + j];
-  double b = Srow[qq * LDR + NM];
+  // Back substitution in the 2-D layout (oracle lu_solve_x: x_k = b_k · (1 / u_kk), then
+  // b_q ← fma(−u_qk, x_k, b_q) for the positions q < k, k descending).  rh is replicated
+  // over the four DPP rows and every lane takes the same fma with column k of U, which
+  // ds_bpermute hands it from DPP row Qk (U is final: fetched two steps ahead, off the
+  // chain); positions ≥ k are solved already, so their (dead) rh may take the fma too.
+  // The chain per step is a readlane, a product and an fma; U never goes to LDS.
   double x = 0.0;
-#pragma unroll
-  for (int k = NM - 1; k >= 0; --k) {
-    const double xk = bcast(b, k) * bcast(rpv, k);  // position k's x, i.e. x of column k
-    if (ln == k) x = xk;
-    if (ln < k) b = fma(-u[k], xk, b);
-  }
+  lu2d_backsub<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, rpv, ln, x);
   dz = x;  // x_k = δ of column k: lane k holds unknown k
   return true;
 }
