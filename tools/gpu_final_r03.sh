@@ -5,6 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/final
 mkdir -p $O
+timeout -k 10 120 ./tools/nl_phase tools/ubench_data/nl_t2_stamps6.hsaco mcpx_nl_solve_schur tools/ubench_data/theta_lane_t2_b1024.bin 40 50 10 1024 64 6 > $O/phase_c4_6.txt 2>&1 || exit 2
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 3
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 4
 timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err || exit 5

@@ -56,18 +56,19 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(st.data(), stamps, st.size() * 8, hipMemcpyDeviceToHost);
   (void)hipMemcpy(nw.data(), newton, B * 4, hipMemcpyDeviceToHost);
   (void)hipMemcpy(stt.data(), status, B * 4, hipMemcpyDeviceToHost);
-  const char* nm[] = {"eval+F+kkt", "schur prep+form", "LU (rest)", "dy/ds+linesearch+update", "LU elimination (2-D)"};
+  const char* nm[] = {"eval+F+kkt", "schur prep+form", "LU (rest)", "dy/ds+linesearch+update", "LU elimination (2-D)", "2-D LU rejected (count)"};
   for (int grp = 0; grp < 2; ++grp) {  // solved, failed
-    double tot[5] = {0, 0, 0, 0, 0}, steps = 0; int cnt = 0, mx = 0;
+    double tot[6] = {0, 0, 0, 0, 0, 0}, steps = 0; int cnt = 0, mx = 0;
     for (int b = 0; b < B; ++b) {
       if ((stt[b] != 0) != (grp == 1)) continue;
       for (int i = 0; i < NST; ++i) tot[i] += st[(size_t)b * NST + i];
       steps += nw[b]; ++cnt; mx = nw[b] > mx ? nw[b] : mx;
     }
-    const double all = tot[0] + tot[1] + tot[2] + tot[3] + tot[4];
+    const double all = tot[0] + tot[1] + tot[2] + tot[3] + (NST > 4 ? tot[4] : 0.0);
     printf("[%s] B=%d kernel %.3f ms  %s: %d instances, newton mean %.1f max %d, cycles per Newton step %.0f\n", kname,
            B, ms, grp ? "failed" : "solved", cnt, cnt ? steps / cnt : 0.0, mx, steps ? all / steps : 0.0);
-    for (int i = 0; i < NST; ++i) printf("  %-26s %5.1f%%  %8.0f cyc/step\n", nm[i], all ? 100 * tot[i] / all : 0.0, steps ? tot[i] / steps : 0.0);
+    for (int i = 0; i < (NST > 5 ? 5 : NST); ++i) printf("  %-26s %5.1f%%  %8.0f cyc/step\n", nm[i], all ? 100 * tot[i] / all : 0.0, steps ? tot[i] / steps : 0.0);
+    if (NST > 5) printf("  guessed 2-D LU rejected on %.2f %% of the steps\n", steps ? 100.0 * tot[5] / steps : 0.0);
   }
   return 0;
 }
