@@ -8,7 +8,9 @@
 // an atomic work queue (grid = the resident workgroups, so imbalance between
 // instances — 12 to 931 Newton steps — evens out).  Per workgroup slot the host
 // allocates a workspace in HBM: the linear system [K | rhs] row-major (ld ≥ NS+1)
-// and, for the nonlinear family, the generated Jacobian blocks.
+// and, for the nonlinear family, the generated Jacobian blocks.  Systems of at most
+// MCPX_VR_MAX rows skip the [K | rhs] workspace: their entries go straight into the
+// registers of the register-resident LU (lu_vr.hpp), same arithmetic.
 //
 // The Newton system is factored by a right-looking blocked LU with partial
 // pivoting that reproduces oracle/ipm_oracle.c::lu_solve bit for bit:

@@ -10,8 +10,9 @@
 // it through the slot's HBM workspace at every panel (the trailing update reads and
 // writes the whole trailing matrix once per 16 columns), while here its entries are
 // computed straight into the VGPRs of the workgroup's WG threads, in the MFMA
-// accumulator layout, and the matrix never touches memory.  Tile (ti, tj) of 16×16 (rows 16ti.., columns 16tj.., right-hand sides
-// as trailing columns) belongs to wave t mod NWAVE with t = tj·R + ti (column-major:
+// accumulator layout, and the matrix never touches memory.  Tile (ti, tj) of 16×16
+// (rows 16ti.., columns 16tj.., right-hand sides as trailing columns) belongs to wave
+// t mod NWAVE with t = tj·R + ti (column-major:
 // every column tile spreads over the waves, so each panel's trailing update is
 // balanced); in it lane (lr, lc) holds rows 16ti + lr + 4e (e < 4) of column 16tj + lc,
 // the f64 MFMA's C layout.  Only the panel (all rows × 16 columns), the panel's U12 rows

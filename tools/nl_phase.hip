@@ -58,7 +58,7 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(stt.data(), status, B * 4, hipMemcpyDeviceToHost);
   const char* nm[] = {"eval+F+kkt", "schur prep+form", "LU (rest)", "dy/ds+linesearch+update", "LU elimination (2-D)", "2-D LU rejected (count)"};
   for (int grp = 0; grp < 2; ++grp) {  // solved, failed
-    double tot[6] = {0, 0, 0, 0, 0, 0}, steps = 0; int cnt = 0, mx = 0;
+    double tot[8] = {0, 0, 0, 0, 0, 0, 0, 0}, steps = 0; int cnt = 0, mx = 0;
     for (int b = 0; b < B; ++b) {
       if ((stt[b] != 0) != (grp == 1)) continue;
       for (int i = 0; i < NST; ++i) tot[i] += st[(size_t)b * NST + i];
@@ -69,6 +69,8 @@ int main(int argc, char** argv) {
            B, ms, grp ? "failed" : "solved", cnt, cnt ? steps / cnt : 0.0, mx, steps ? all / steps : 0.0);
     for (int i = 0; i < (NST > 5 ? 5 : NST); ++i) printf("  %-26s %5.1f%%  %8.0f cyc/step\n", nm[i], all ? 100 * tot[i] / all : 0.0, steps ? tot[i] / steps : 0.0);
     if (NST > 5) printf("  guessed 2-D LU rejected on %.2f %% of the steps\n", steps ? 100.0 * tot[5] / steps : 0.0);
+    if (NST > 7) printf("  of LU (rest): 2-D back substitution %.0f, searched-LU fallback %.0f cyc/step\n",
+                        steps ? tot[6] / steps : 0.0, steps ? tot[7] / steps : 0.0);
   }
   return 0;
 }
