@@ -1,7 +1,8 @@
 // Workgroup-per-instance kernels of the QP and affine families (ipm_wg_impl.hpp):
-// MCPX_LINSOLVE_REDUCED / _DENSE at vector dimension buckets 128 … 768.  A system of at
-// most MCPX_VR_MAX rows in a larger bucket (REDUCED at KKT 256: n + m = 192) takes the
-// instance whose LU holds the matrix in registers (NS = MCPX_VR_MAX, lu_vr.hpp).
+// MCPX_LINSOLVE_REDUCED / _DENSE at vector dimension buckets 128 … 768.  Bucket 128 and
+// the systems of at most MCPX_VR_MAX rows in bucket 256 (REDUCED at KKT 256: n + m = 192)
+// take the register-resident LU (lu_vr.hpp); those kernels are compiled in their own
+// unit, ipm_inst_wg_vr.hip (they dominate the build), and reached through ipm_wg_vr_kernel.
 #include "ipm_wg_impl.hpp"
 
 namespace mcpx {
@@ -14,11 +15,8 @@ __global__ __launch_bounds__(wg::kThreads) void ipm_wg_kernel_t(const wg::WgArgs
 namespace {
 template <int FAMILY, int SOLVER>
 const void* pick(int nv, int ns) {
-#if MCPX_VR_MAX > 0
-  if (nv == 256 && ns <= MCPX_VR_MAX) return (const void*)&ipm_wg_kernel_t<FAMILY, SOLVER, 256, MCPX_VR_MAX>;
-#endif
+  if (nv == 128 || (nv == 256 && ns <= MCPX_VR_MAX)) return ipm_wg_vr_kernel(FAMILY, SOLVER, nv);
   switch (nv) {
-    case 128: return (const void*)&ipm_wg_kernel_t<FAMILY, SOLVER, 128>;
     case 256: return (const void*)&ipm_wg_kernel_t<FAMILY, SOLVER, 256>;
     case 512: return (const void*)&ipm_wg_kernel_t<FAMILY, SOLVER, 512>;
     case 768: return (const void*)&ipm_wg_kernel_t<FAMILY, SOLVER, 768>;

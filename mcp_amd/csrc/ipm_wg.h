@@ -56,6 +56,9 @@ constexpr int kDimBuckets[4] = {128, 256, 512, 768};
 // ns: rows of the factored system (a system of at most MCPX_VR_MAX rows is factored in
 // registers, lu_vr.hpp).
 const void* ipm_wg_kernel(int family, int solver, int nv, int ns);
+// The register-resident ones (ipm_inst_wg_vr.hip): bucket 128, and bucket 256 for
+// systems of at most MCPX_VR_MAX rows; nullptr otherwise.
+const void* ipm_wg_vr_kernel(int family, int solver, int nv);
 hipError_t launch_ipm_wg(int family, int solver, int nv, int ns, const wg::WgArgs& a, int grid, hipStream_t st);
 // Sensitivity kernels of the QP and affine families beyond the one-wave kernels'
 // 64 rows (sens_inst_wg.hip): VJP (jvp = false) or JVP at vector dimension
