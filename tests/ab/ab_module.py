@@ -3,7 +3,7 @@
     python tests/ab/ab_module.py build NAME CSRC_DIR [T]   # CPU: module text of T (default 2) + CSRC_DIR headers
     python tests/ab/ab_module.py run NAME... [--T T] [--B B]  # GPU: time each, compare with the oracle
 
-Variants are throwaway code objects under tools/abx/ (not kept in the tree); the
+Variants are throwaway code objects under tools/abx/ or $MCPX_AB_OUT (not kept in the tree); the
 generated text is the product's (mcp_amd/codegen.py), only the kernel headers differ."""
 import os, subprocess, sys, time
 import numpy as np
