@@ -53,7 +53,11 @@
 extern "C" {
 #endif
 
-#define MCPX_VERSION 10600 /* 1.6.0 */
+/* 2.0.0: mcpx_out gained the trailing fail_reason pointer (1.6), which changes the
+ * struct's size and layout: a caller built against a 1.x header passes a shorter
+ * struct, so the major version moved.  Callers check mcpx_version() / 10000 against
+ * MCPX_VERSION / 10000 before the first call (mcp_amd/_lib.py does). */
+#define MCPX_VERSION 20000 /* 2.0.0 */
 
 /* error codes */
 #define MCPX_OK 0
@@ -237,9 +241,10 @@ int mcpx_solve_batch_device(const mcpx_desc* desc, const double* theta,
  * ChainRulesCore's ZeroTangent).  Output: dtheta [B*p] (p = mcpx_theta_dim,
  * dense stride p, the family's θ layout), status [B] or NULL.
  * n + 2m <= MCPX_MAX_KKT_DIM runs one wave per instance (the system in registers),
- * larger systems up to MCPX_MAX_WG_KKT_DIM one workgroup per instance (the
- * system in an HBM workspace, blocked LU with MFMA trailing updates); both give
- * the same bits. */
+ * larger systems up to MCPX_MAX_WG_KKT_DIM one workgroup per instance: blocked LU
+ * with partial pivoting and MFMA trailing updates, on a per-slot HBM workspace
+ * holding [K | rhs] (the register-resident LU of the solve kernels, lu_vr.hpp, is
+ * not used by the sensitivity kernels); both give the same bits. */
 int mcpx_vjp_batch(const mcpx_desc* desc, const double* theta, const double* x, const double* y,
                    const double* s, const double* gx, const double* gy, const double* gs,
                    int num_devices, double* dtheta, int32_t* status);

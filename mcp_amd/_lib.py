@@ -33,6 +33,9 @@ EXPORTS = ("mcpx_version", "mcpx_last_error", "mcpx_default_params", "mcpx_theta
            "mcpx_jvp_batch_module", "mcpx_jvp_batch_module_device", "mcpx_solve_vjp_batch_device")
 
 
+ABI_MAJOR = 2  # include/mcpx.h MCPX_VERSION / 10000
+
+
 def lib():
     """Load libmcpx.so (building it first if only the sources are present)."""
     global _lib
@@ -43,6 +46,8 @@ def lib():
         _build.build()
     L = C.CDLL(LIB_PATH)
     L.mcpx_version.restype = C.c_int
+    if L.mcpx_version() // 10000 != ABI_MAJOR:  # mcpx_out's layout is part of the major version
+        raise RuntimeError(f"{LIB_PATH}: ABI {L.mcpx_version()} does not match this package's major {ABI_MAJOR}")
     L.mcpx_last_error.restype = C.c_char_p
     L.mcpx_default_params.argtypes = [C.POINTER(_abi.Params)]
     L.mcpx_theta_dim.restype = C.c_int64

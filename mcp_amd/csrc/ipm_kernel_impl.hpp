@@ -836,7 +836,7 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
 // The rrule pullback fused into the solve kernel's epilogue (defined in
 // sens_kernel_impl.hpp; only the FUSE instantiations of ipm_inst_fused.hip use it).
 template <int NV, int FAMILY, int NT, bool LU>
-__device__ __forceinline__ void fused_vjp(const KernelArgs& A, int64_t inst, int ln, int n, int m, double z, double s,
+__device__ __forceinline__ bool fused_vjp(const KernelArgs& A, int64_t inst, int ln, int n, int m, double z, double s,
                                           const double* th, const double* ta, int lda, bool msym,
                                           double* const (&lds)[5]);
 
@@ -1144,6 +1144,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
     reason |= MCPX_FAIL_MAX_OUTER;
   }
 
+  if constexpr (FUSE > 0) {
+    static_assert(RED && FAMILY == MCPX_FAMILY_QP, "the fused pullback follows the QP REDUCED / SCHUR lane layout");
+    // The pullback runs before the outputs are written: an instance the fast pass defers
+    // must leave x/y/s untouched, since pass 2 re-solves it from x0/y0/s0, which a caller
+    // may have aliased to the output buffers (warm start in place).
+    // The pullback's Schur path reuses the solve's A block (LDS copy) and its M-symmetry test
+    // (opaque sizes: with constant ones the pullback's loops unroll into spills)
+    double* const lds[5] = {zs, sD, sT, sB, sF};
+    const bool done = fused_vjp<FUSE, FAMILY, (NMAX + 15) / 16, PASS != 1>(
+        args, inst, lane, opaque(n0), opaque(m0), z, s, th0, LDSA ? (const double*)sA : th0 + n0 * n0,
+        LDSA ? LDA : m0, spd_try, lds);
+    if (!done) {  // PASS 1 only (the LU pass always completes)
+      if (lane == 0) args.status[inst] = STATUS_DEFERRED;
+      return;
+    }
+  }
+
   // ---- outputs (:121) -----------------------------------------------------
   const int n = n0, m = m0;
   const bool rx = lane < n, ry = lane >= n && lane < n + m;
@@ -1177,15 +1194,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
     args.status[inst] = status;
     if (args.newton_iters) args.newton_iters[inst] = newton;
     if (args.fail_reason) args.fail_reason[inst] = (uint8_t)reason;
-  }
-  if constexpr (FUSE > 0) {
-    static_assert(RED && FAMILY == MCPX_FAMILY_QP, "the fused pullback follows the QP REDUCED / SCHUR lane layout");
-    // the pullback's Schur path reuses the solve's A block (LDS copy) and its M-symmetry test
-    // (opaque sizes: with constant ones the pullback's loops unroll into spills)
-    double* const lds[5] = {zs, sD, sT, sB, sF};
-    fused_vjp<FUSE, FAMILY, (NMAX + 15) / 16, PASS != 1>(args, inst, lane, opaque(n), opaque(m), z, s, th0,
-                                                         LDSA ? (const double*)sA : th0 + n * n, LDSA ? LDA : m,
-                                                         spd_try, lds);
   }
 }
 

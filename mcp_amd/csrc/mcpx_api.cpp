@@ -816,8 +816,9 @@ int sens_shard(bool jvp, int dev, const mcpx_desc* d, const mcpx::SensArgs& a0, 
 }
 
 // Shards of a host-buffer call: one per device, or MCPX_HOST_SHARDS = k contiguous shards
-// over the visible devices round-robin (one host thread each; a test knob that runs the
-// multi-device path on a box with fewer devices).
+// over the caller's (clamped) devices round-robin — shard g runs on device g mod
+// num_devices, never on a device the caller did not ask for (one host thread each; a test
+// knob that runs the multi-device path on a box with fewer devices).
 int host_shards(int num_devices, int64_t batch) {
   const char* e = std::getenv("MCPX_HOST_SHARDS");
   const int k = e ? std::atoi(e) : 0;
@@ -834,7 +835,8 @@ int sens_host(bool jvp, const mcpx_desc* d, const mcpx::SensArgs& a, const SensP
   if (avail < 1) return fail(MCPX_ENODEV, "no HIP device visible");
   if (num_devices <= 0 || num_devices > avail) num_devices = avail;
   if ((int64_t)num_devices > d->batch) num_devices = (int)d->batch;
-  num_devices = host_shards(num_devices, d->batch);
+  const int devs = num_devices;
+  num_devices = host_shards(devs, d->batch);
   std::vector<int64_t> start(num_devices + 1, 0);
   for (int g = 0; g < num_devices; ++g)
     start[g + 1] = start[g] + d->batch / num_devices + (g < d->batch % num_devices ? 1 : 0);
@@ -843,7 +845,7 @@ int sens_host(bool jvp, const mcpx_desc* d, const mcpx::SensArgs& a, const SensP
   std::vector<std::thread> th;
   for (int g = 0; g < num_devices; ++g)
     th.emplace_back([&, g] {
-      rcs[g] = sens_shard(jvp, g % avail, d, a, plan, theta, x, y, s, gx, gy, gs, tdot, out, status, start[g],
+      rcs[g] = sens_shard(jvp, g % devs, d, a, plan, theta, x, y, s, gx, gy, gs, tdot, out, status, start[g],
                           start[g + 1] - start[g]);
       if (rcs[g]) errs[g] = g_err;
     });
@@ -1000,8 +1002,9 @@ int solve_host_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, c
   if (avail < 1) return fail(MCPX_ENODEV, "no HIP device visible");
   if (num_devices <= 0 || num_devices > avail) num_devices = avail;
   if ((int64_t)num_devices > d->batch) num_devices = (int)d->batch;
-  num_devices = host_shards(num_devices, d->batch);
-  // contiguous shards: shard g (device g mod the visible count) gets ⌊B/G⌋ (+1 for g < B mod G)
+  const int devs = num_devices;
+  num_devices = host_shards(devs, d->batch);
+  // contiguous shards: shard g (device g mod devs) gets ⌊B/G⌋ (+1 for g < B mod G)
   std::vector<int64_t> start(num_devices + 1, 0);
   for (int g = 0; g < num_devices; ++g)
     start[g + 1] = start[g] + d->batch / num_devices + (g < d->batch % num_devices ? 1 : 0);
@@ -1011,7 +1014,7 @@ int solve_host_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, c
   std::vector<std::thread> th;
   for (int g = 0; g < num_devices; ++g)
     th.emplace_back([&, g] {
-      rcs[g] = solve_shard(g % avail, d, theta, x0, y0, s0, prm, o, start[g], start[g + 1] - start[g], mod);
+      rcs[g] = solve_shard(g % devs, d, theta, x0, y0, s0, prm, o, start[g], start[g + 1] - start[g], mod);
       if (rcs[g]) errs[g] = g_err;
     });
   for (auto& t : th) t.join();

@@ -448,11 +448,14 @@ __global__ __launch_bounds__(64) void vjp_kernel(const SensArgs A) {
 // The pullback fused into the solve kernel's epilogue (ipm_solve_kernel<…, FUSE = NV>):
 // the solve's lane layout (lanes [0, n) x, [n, n+m) y with s in `s`) into LDS, the
 // cotangent a ⊙ z + b of KernelArgs, vjp_instance with register width NV ≥ n + m.
-// LU = false (fast pass): an instance the Schur path cannot take is deferred to the
-// second pass, which solves it again (same bits) and pulls back with the LU fallback.
-// lds: five 64-double LDS arrays of the solve kernel, dead once its outputs are written.
+// LU = false (fast pass): returns false, having written nothing, when the Schur path cannot
+// take the instance; the caller then defers it to the second pass, which solves it again
+// (same bits) and pulls back with the LU fallback.  The caller runs this BEFORE writing the
+// solve's outputs, so a deferred instance leaves x/y/s untouched and a warm start read from
+// the output buffers (x0 = out.x, the receding-horizon pattern) is still intact for pass 2.
+// lds: five 64-double LDS arrays of the solve kernel, dead once its Newton loop is done.
 template <int NV, int FAMILY, int NT, bool LU>
-__device__ __forceinline__ void fused_vjp(const KernelArgs& A, int64_t inst, int ln, int n, int m, double z, double s,
+__device__ __forceinline__ bool fused_vjp(const KernelArgs& A, int64_t inst, int ln, int n, int m, double z, double s,
                                           const double* th, const double* ta, int lda, bool msym,
                                           double* const (&lds)[5]) {
   double* const zs = lds[0];
@@ -475,7 +478,7 @@ __device__ __forceinline__ void fused_vjp(const KernelArgs& A, int64_t inst, int
   const bool done = vjp_instance<NV, FAMILY, NT, LU>(th, zs, lam, gsv, g, ln, n, m, A.vjp_dtheta + inst * p,
                                                      A.vjp_status ? A.vjp_status + inst : nullptr, ta, lda, msym,
                                                      lds[3], lds[4]);
-  if (!done && ln == 0) A.status[inst] = STATUS_DEFERRED;
+  return done;
 }
 
 template <int NMAX, int FAMILY>

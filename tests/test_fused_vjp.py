@@ -161,3 +161,41 @@ def test_gpu_solve_vjp_asymmetric_m_takes_the_lu_pass(gpu, oracle_lib):
     x, y, s = (ref[f].cpu().numpy() for f in ("x", "y", "s"))
     odth, ost = oracle_lib.vjp_batch(0, n, m, th_h, x, y, s, 2.0 * x, 2.0 * y, None)
     assert _same(dth.cpu().numpy(), odth) and _same(st.cpu().numpy(), ost)
+
+
+@pytest.mark.gpu
+def test_gpu_solve_vjp_warm_start_in_place(gpu):
+    """Warm start read from the output buffers (x0 = out.x, y0 = out.y, s0 = out.s, the
+    receding-horizon pattern) on instances the fused fast pass defers at the pullback
+    (y < 0 at the returned iterate: the Schur pullback does not apply, so pass 2 solves
+    them again from x0/y0/s0).  The fast pass must not have overwritten those buffers
+    first: the bits equal the composed calls on separate warm-start buffers."""
+    import torch
+
+    from mcp_amd.batch import alloc_device_outputs, solve_batch_device, solve_vjp_batch_device, vjp_batch_device
+
+    rng = np.random.default_rng(2024)
+    n, m, B = 16, 8, 256
+    dev = torch.device("cuda", 0)
+    th = torch.from_numpy(generate_random_parameter(rng, n, m, 0.0, batch=B)).to(dev)
+    x0 = torch.from_numpy(rng.standard_normal((B, n))).to(dev)
+    yh = rng.uniform(0.5, 2.0, (B, m))
+    yh[::2] *= -1.0  # every other instance starts (and stays) with y < 0
+    y0 = torch.from_numpy(yh).to(dev)
+    s0 = torch.from_numpy(rng.uniform(0.5, 2.0, (B, m))).to(dev)
+    kw = dict(tol=1e-6, linear_solver="schur", max_outer_iters=4)
+    ref = solve_batch_device(0, n, m, th, alloc_device_outputs(B, n, m, dev), x0=x0, y0=y0, s0=s0, **kw)
+    rdth, rst = vjp_batch_device(0, n, m, th, ref["x"], ref["y"], ref["s"], 2.0 * ref["x"], 2.0 * ref["y"])
+    out = alloc_device_outputs(B, n, m, dev)
+    out["x"].copy_(x0)
+    out["y"].copy_(y0)
+    out["s"].copy_(s0)
+    out, dth, st = solve_vjp_batch_device(0, n, m, th, out, ct=(2.0, 2.0, 0.0), x0=out["x"], y0=out["y"],
+                                          s0=out["s"], **kw)
+    torch.cuda.synchronize()
+    ry = ref["y"].cpu().numpy()
+    assert (ry < 0).any(axis=1).sum() > 0  # some instances do take the deferred pullback
+    assert not np.array_equal(ref["x"].cpu().numpy(), x0.cpu().numpy())  # and their solves moved x
+    for f in QP_FIELDS:
+        assert _same(out[f].cpu().numpy(), ref[f].cpu().numpy()), f
+    assert _same(dth.cpu().numpy(), rdth.cpu().numpy()) and _same(st.cpu().numpy(), rst.cpu().numpy())
