@@ -481,7 +481,7 @@ def main_lane_change(a, world, rank, local, dist, pl):
         coracle.build()
         th = a.cpu_threads or host_cpus()["nproc"]
         cb = cpu_baseline(lambda k, t: coracle.solve_batch_nl(mcp.nl, theta_host[:k], tol=a.tol, linear_solver=ls,
-                                                              nthreads=t),
+                                                              kernel=a.kernel, nthreads=t),
                           B, a, th, "C oracle with the generated host G/H code (same algorithm and linear solver)",
                           per_thread=256 if a.lane_change <= 2 else 4)
         r = cb.pop("_result")

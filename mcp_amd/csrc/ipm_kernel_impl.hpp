@@ -52,9 +52,24 @@
 #define MCPX_LDS_A 1
 #endif
 
+// kkt and ϵ re-read into SGPRs after each update (A/B knob).
+#ifndef MCPX_SREG_KKT
+#define MCPX_SREG_KKT 0
+#endif
+
+// θ loads in flight per lane in the SCHUR residual dot products (A/B knob).
+#ifndef MCPX_RES_BATCH
+#define MCPX_RES_BATCH 8
+#endif
+
 // Waves per SIMD the register allocator targets in the SCHUR fast pass (A/B knob).
 #ifndef MCPX_FAST_WAVES
 #define MCPX_FAST_WAVES 5
+#endif
+
+// Dispatch-order priority levels (A/B knob; 0 = off): see ipm_solve_kernel.
+#ifndef MCPX_PRIO
+#define MCPX_PRIO 0
 #endif
 
 // Diagnostic phase stamps (tools/phase_profile.hip builds with MCPX_STAMPS=1;
@@ -158,6 +173,14 @@ __device__ __forceinline__ double rcp_fast(double b) {
 __device__ __forceinline__ double rcp_uniform(double b) {
   if (__builtin_expect(rcp_fast_ok(b), 1)) return rcp_fast(b);
   return 1.0 / b;
+}
+
+// A wave-uniform double moved to SGPRs (readfirstlane of both halves): keeps loop-carried
+// uniform values (kkt, ϵ) out of the VGPR budget.
+__device__ __forceinline__ double uniform_f64(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
 }
 
 // NaN-propagating max (Julia `max`, as in norm(F, Inf), src/solver.jl:107)
@@ -344,9 +367,10 @@ __device__ __forceinline__ void eliminate_row(double (&a)[NMAX], double& rhs, in
 #ifndef MCPX_LU_NO_SPEC
 #define MCPX_LU_NO_SPEC 0
 #endif
-// RCP (the SCHUR step of generated nonlinear modules, oracle lu_solve_x rcp): multipliers
-// a_ik · (1 / piv) and back substitution x_k = b_p · (1 / u_kk), one correctly rounded
-// reciprocal (rcp_uniform) per pivot.
+// RCP (the SCHUR step of generated nonlinear modules, oracle lu_solve_x rcp = 2): Gauss-Jordan
+// with the same pivot search — multipliers a_ik · (1 / piv), one correctly rounded reciprocal
+// (rcp_uniform) per pivot, every row but the pivot row updated, the pivot row with
+// multiplier +0 (l = −0: fma(+0, u, a)) — and x_k = b_p · (1 / u_pk), no back substitution.
 template <int NMAX, bool RCP = false>
 __device__ __forceinline__ bool lu_solve_rows_core(double (&a)[NMAX], double rhs, int N, int ln, double& dz,
                                                    int& pk, bool spec, bool& miss) {
@@ -403,23 +427,29 @@ __device__ __forceinline__ bool lu_solve_rows_core(double (&a)[NMAX], double rhs
     double l;
     if constexpr (RCP) {
       const double rp = rcp_uniform(piv);
-      if (ln == k) rcpd = rp;
-      l = ak * rp;
+      if (ln == p) rcpd = rp;
+      l = (ln == p) ? -0.0 : ak * rp;  // Gauss-Jordan: the pivot row takes fma(+0, u, a)
+      eliminate_row<NMAX>(a, rhs, k, l, 1ull << p, true);
     } else {
       l = ak / piv;
+      eliminate_row<NMAX>(a, rhs, k, l, 1ull << p, (rem >> ln) & 1ull);
     }
-    eliminate_row<NMAX>(a, rhs, k, l, 1ull << p, (rem >> ln) & 1ull);
   }
   if (spec && ballot(viol)) miss = true;
   if (singular || miss) return false;
+  if constexpr (RCP) {  // x_k = b_p · (1 / u_pk) in lane p = pk of lane k
+    const double xp = rhs * rcpd;
+    const int lo = __builtin_amdgcn_ds_bpermute(pk << 2, __double2loint(xp));
+    const int hi = __builtin_amdgcn_ds_bpermute(pk << 2, __double2hiint(xp));
+    dz = __hiloint2double(hi, lo);
+    return true;
+  }
   dz = 0.0;
 #pragma clang loop unroll(full)
   for (int k = NMAX - 1; k >= 0; --k) {
     if (k < N) {
       const int p = __builtin_amdgcn_readlane(pk, k);
-      double xk;
-      if constexpr (RCP) xk = bcast(rhs, p) * bcast(rcpd, k);
-      else xk = bcast(rhs / a[k], p);
+      const double xk = bcast(rhs / a[k], p);
       if (ln == k) dz = xk;
       if (my_step < k) rhs = fma(-a[k], xk, rhs);
     }
@@ -892,6 +922,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   if constexpr (PASS == 2) {
     if (__builtin_amdgcn_readfirstlane(args.status[blockIdx.x]) != STATUS_DEFERRED) return;
   }
+  if constexpr (MCPX_PRIO > 0) {
+    // VALU issue on a SIMD is arbitrated by priority, then age: with equal priorities the
+    // oldest resident wave wins, so the waves dispatched last — the ones that set the end of
+    // a launch that needs more than one round of residency — get the leftover issue slots.
+    // Static priority graded by dispatch order (blockIdx): quarter q of the grid runs at q.
+    const unsigned q = (unsigned)(((uint64_t)blockIdx.x * MCPX_PRIO) / gridDim.x);
+    if (q == 1) __builtin_amdgcn_s_setprio(1);
+    else if (q == 2) __builtin_amdgcn_s_setprio(2);
+    else if (q >= 3) __builtin_amdgcn_s_setprio(3);
+  }
   __shared__ double zs[64];
   __shared__ double sD[SCH ? 64 : 1], sT[SCH ? 64 : 1];  // SCHUR: D_k⁻¹, ty_k
   __shared__ double sB[SCH ? 64 : 1];  // rr, restored for the LU fallback
@@ -992,7 +1032,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       // quotient-per-use form costs (8 of them in the Schur K-loop).
       double rw = 1.0, Di = 1.0, ryr = 0.0;
       if constexpr (SCH) {
-        qp_residuals<8>(th, ta, lda, zs, ln, n, m, eps, s, F, Fc);
+        qp_residuals<MCPX_RES_BATCH>(th, ta, lda, zs, ln, n, m, eps, s, F, Fc);
         rhs = -F;
         if (rh) {  // eliminate δs_k (pivot w_k) and then δy_k (pivot D_k)
           w = zs[ln] + tol;
@@ -1131,12 +1171,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         if (rx || rs) z = z + as * dz;
         if (ry) z = z + ay * dz;
       }
-      kkt = kkt_step;  // :107
+      kkt = MCPX_SREG_KKT ? uniform_f64(kkt_step) : kkt_step;  // :107
       MCPX_STAMP(5);
       ++inner;         // :108
       ++newton;
     }
     eps *= (status == 0) ? args.tight[inner] : args.loose[inner];  // :111-113
+    if (MCPX_SREG_KKT) eps = uniform_f64(eps);
     ++outer;                                                        // :114
   }
   if (outer == args.max_outer) {  // :117-119

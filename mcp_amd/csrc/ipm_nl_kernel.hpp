@@ -55,71 +55,88 @@ constexpr int rows_of(int solver) {
   return solver == MCPX_LINSOLVE_DENSE ? N : (solver == MCPX_LINSOLVE_REDUCED ? n + m : n);
 }
 
-// ---- 2-D Gauss elimination of the one-wave SCHUR kernel ------------------------------
-// LU of [S | rr] with the previous Newton step's pivot sequence (lane k of pk = row p_k)
-// as the guess, in the matrix-core layout of the QP Gauss-Jordan (csrc/ipm_kernel_impl.hpp,
-// gj2d_spd): lane (lr, lc) holds position q = lc + 16J (J < NJ) at columns lr + 4c (c < NCB),
-// position q being row p_q, so step k's pivot is position k and its row reaches every lane
-// through DPP row_newbcast operands of the fmas; the pivot column goes to every lane by
-// ds_bpermute.  Multipliers a_qk · (1 / piv) (oracle lu_solve_x, rcp).  Finished halves are
-// skipped; rows of the pivot half at or before the pivot take the update with multiplier +0
-// (their lanes are the DPP sources); columns ≤ k of a straddling 4-column block are updated
-// too and never read again.  Each step checks the first-max rule against the guess on the
-// 64-bit |a| keys (a NaN entry counts as a violation); a violation or a zero / NaN guessed
-// pivot returns false with Srow untouched, for the searched LU.  On success the U rows go to
-// Srow and the substitution x_k = b_k · (1 / u_kk) runs lane per row; dz = x of row `ln`.
+// ---- 2-D Gauss-Jordan of the one-wave SCHUR kernel ------------------------------------
+// Gauss-Jordan with partial pivoting of [S | rr] (oracle lu_solve_x, rcp = 2) with the
+// previous Newton step's pivot sequence (lane k of pk = row p_k) as the guess, in the
+// matrix-core layout of the QP Gauss-Jordan (csrc/ipm_kernel_impl.hpp, gj2d_spd): lane
+// (lr, lc) holds position q = lc + 16J (J < NJ) at columns lr + 4c (c < NCB), position q
+// being row p_q, so step k's pivot is position k and its row reaches every lane through DPP
+// row_newbcast operands of the fmas; the pivot column goes to every lane by ds_bpermute.
+// Multipliers a_qk · (1 / piv); every position but the pivot's takes the update, the pivot
+// row itself with multiplier +0 (its lanes are the DPP sources; the oracle does the same);
+// columns ≤ k of a straddling 4-column block are updated too and never read again.  Each
+// step checks the first-max rule against the guess over the remaining positions (a NaN
+// entry counts as a violation); a violation or a zero / NaN / out of
+// range guessed pivot returns false, Srow untouched, for the searched Gauss-Jordan.  On
+// success x_k = b_k · (1 / u_kk) needs no substitution: lane k holds position k's rhs
+// (rh[lr]) and 1 / u_kk.  (The LU with back substitution this replaced spent a third of a
+// failing lane-change game's Newton step in the 40-step dependent substitution chain.)
 template <int NM>
 struct Lu2d {
   static constexpr int NJ = (NM + 15) / 16, NCB = (NM + 3) / 4;
 };
 
-// Step K with one step of lookahead: `piv` (uniform) and `col` (column K by position,
-// from ds_bpermute) were fetched by step K − 1 right after it updated column K, so their
-// LDS latency hides behind the rest of that step's update.  Step K updates the column
-// block of column K + 1 first, fetches pivot K + 1 and its column, then updates the other
-// blocks.  Each entry still takes the same fma in the same order.  1 / piv is the
-// uniform fast reciprocal with no branch: a pivot that is zero, NaN or outside its exact
-// range only sets `bad`, the remaining steps run on (discarded) values, and the caller
-// falls back to the searched LU.
+// Lanes 0..15 (DPP row 0; every DPP row holds the same column entries) whose position
+// q = lane + 16J is still remaining at step K: q > K, q < NM.
+template <int NM, int K, int J>
+constexpr uint64_t remaining_lanes() {
+  uint64_t m = 0;
+  for (int l = 0; l < 16; ++l)
+    if (l + 16 * J > K && l + 16 * J < NM) m |= 1ull << l;
+  return m;
+}
+
+// Step K with one step of lookahead: `piv` (uniform), its reciprocal `rp` and `col` (column
+// K by position, from ds_bpermute) were produced by step K − 1 right after it updated column
+// K, so the LDS latency and the reciprocal's 7-deep dependent chain hide behind the rest of
+// that step's update.  Step K updates the column block of column K + 1 first, fetches pivot
+// K + 1, starts its reciprocal and fetches its column, then updates the other blocks.  Each
+// entry still takes the same fma in the same order.  1 / piv is the uniform fast reciprocal
+// with no branch: a pivot that is zero, NaN or outside its exact range only sets `bad`, the
+// remaining steps run on (discarded) values, and the caller falls back to the searched
+// Gauss-Jordan.  The first-max check of the guess is three compares per half into lane
+// masks (|a_qk| > |piv| or NaN; equal with a lower row index), on the remaining positions.
 template <int NM, int K>
 __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
-                                          const int (&pv)[Lu2d<NM>::NJ], int pkk, int ln, uint32_t& viol,
-                                          double& rpv, bool& bad, double& piv, double (&col)[Lu2d<NM>::NJ]) {
+                                          const int (&pv)[Lu2d<NM>::NJ], int pkk, int ln, uint64_t& viol,
+                                          double& rpv, bool& bad, double& piv, double& rp,
+                                          double (&col)[Lu2d<NM>::NJ]) {
   constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
   constexpr int Jk = K >> 4, Rk = K & 15;
   constexpr bool NX = K + 1 < NM;  // a next pivot to fetch
   constexpr int Jn = (K + 1) >> 4, Rn = (K + 1) & 15, Qn = (K + 1) & 3, Cn = (K + 1) >> 2;
   __builtin_amdgcn_sched_barrier(0);  // one step at a time: no step's uniform values hoisted ahead
   const int lc = ln & 15;
-  bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
-  const double rp = rcp_fast(piv);
   if (ln == K) rpv = rp;
-  const int64_t kp = (int64_t)((uint64_t)__double_as_longlong(piv) & 0x7fffffffffffffffull);
+  const double ap = fabs(piv);
   double nlm[NJ];
 #pragma unroll
   for (int J = 0; J < NJ; ++J) {
-    if (J < Jk) continue;
     const double v = col[J];  // a_qk of position q = lc + 16J
     const int q = lc + 16 * J;
-    const bool remq = (q > K) & (q < NM);
-    const int64_t kq = (int64_t)((uint64_t)__double_as_longlong(v) & 0x7fffffffffffffffull);
-    const int64_t d = (kp - (int64_t)(pv[J] < pkk)) - kq;
-    viol |= (uint32_t)((uint64_t)d >> 63) & (uint32_t)remq;
-    nlm[J] = remq ? -(v * rp) : 0.0;
+    constexpr uint64_t REM[4] = {remaining_lanes<NM, K, 0>(), remaining_lanes<NM, K, 1>(),
+                                 remaining_lanes<NM, K, 2>(), remaining_lanes<NM, K, 3>()};
+    if (J >= Jk && REM[J & 3] != 0) {  // the first-max rule over the remaining positions
+      const double av = fabs(v);
+      viol |= (ballot(!(av <= ap)) | (ballot(av == ap) & ballot(pv[J] < pkk))) & REM[J & 3];
+    }
+    // Gauss-Jordan: every position but the pivot's, remaining or not; the pivot row +0
+    nlm[J] = ((q != K) & (q < NM)) ? -(v * rp) : 0.0;
   }
-  if constexpr (NX) {  // column block of column K + 1, then pivot K + 1 and its column
+  if constexpr (NX) {  // column block of column K + 1, then pivot K + 1, its reciprocal and column
 #pragma unroll
     for (int J = 0; J < NJ; ++J)
-      if (J > Jk) fmac_row_bcast<Rk, false>(acc[J][Cn], acc[Jk][Cn], nlm[J]);
+      if (J != Jk) fmac_row_bcast<Rk, false>(acc[J][Cn], acc[Jk][Cn], nlm[J]);
     fmac_row_bcast_self<Rk, false>(acc[Jk][Cn], nlm[Jk]);
     piv = bcast(acc[Jn][Cn], 16 * Qn + Rn);
+    bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
+    rp = rcp_fast(piv);
 #pragma unroll
-    for (int J = 0; J < NJ; ++J)
-      if (J >= Jn) col[J] = bperm_f64_addr(acc[J][Cn], (16 * Qn + lc) << 2);
+    for (int J = 0; J < NJ; ++J) col[J] = bperm_f64_addr(acc[J][Cn], (16 * Qn + lc) << 2);
   }
 #pragma unroll
   for (int J = 0; J < NJ; ++J) {
-    if (J <= Jk) continue;
+    if (J == Jk) continue;
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
       if (4 * c + 3 <= K || (NX && c == Cn)) continue;
@@ -138,59 +155,16 @@ __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::
 template <int NM, int... K>
 __device__ __forceinline__ void lu2d_steps(std::integer_sequence<int, K...>,
                                            double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
-                                           const int (&pv)[Lu2d<NM>::NJ], int pk, int ln, uint32_t& viol, double& rpv,
+                                           const int (&pv)[Lu2d<NM>::NJ], int pk, int ln, uint64_t& viol, double& rpv,
                                            bool& bad) {
   constexpr int NJ = Lu2d<NM>::NJ;
   const int lc = ln & 15;
-  double piv = bcast(acc[0][0], 0), col[NJ];  // pivot 0 and column 0
+  double piv = bcast(acc[0][0], 0), col[NJ];  // pivot 0, its reciprocal and column 0
+  bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
+  double rp = rcp_fast(piv);
 #pragma unroll
   for (int J = 0; J < NJ; ++J) col[J] = bperm_f64_addr(acc[J][0], lc << 2);
-  (lu2d_step<NM, K>(acc, rh, pv, __builtin_amdgcn_readlane(pk, K), ln, viol, rpv, bad, piv, col), ...);
-}
-
-// Column k of U for every lane's positions (lanes (·, lc) get position lc + 16J from DPP row
-// Qk), J ≤ Jk only.
-template <int NM, int K>
-__device__ __forceinline__ void lu2d_ucol(const double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], int ln,
-                                          double (&uc)[Lu2d<NM>::NJ]) {
-  constexpr int NJ = Lu2d<NM>::NJ, Jk = K >> 4, Qk = K & 3, Ck = K >> 2;
-  const int addr = (16 * Qk + (ln & 15)) << 2;
-#pragma unroll
-  for (int J = 0; J < NJ; ++J) uc[J] = J <= Jk ? bperm_f64_addr(acc[J][Ck], addr) : 0.0;
-}
-
-template <int NM, int K>
-__device__ __forceinline__ void lu2d_backsub_step(const double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB],
-                                                  double (&rh)[Lu2d<NM>::NJ], double rpv, int ln, double& x,
-                                                  double (&u0)[Lu2d<NM>::NJ], double (&u1)[Lu2d<NM>::NJ],
-                                                  double (&u2)[Lu2d<NM>::NJ]) {
-  constexpr int NJ = Lu2d<NM>::NJ, Jk = K >> 4, Rk = K & 15;
-  __builtin_amdgcn_sched_barrier(0);
-  // u0 = column K (fetched two steps ago); start the fetch of column K − 3 into a free slot
-  double nx[NJ];
-  if constexpr (K >= 3) lu2d_ucol<NM, K - 3>(acc, ln, nx);
-  const double xk = bcast(rh[Jk], Rk) * bcast(rpv, K);  // position K's x (every DPP row holds rh)
-  if (ln == K) x = xk;
-#pragma unroll
-  for (int J = 0; J <= Jk; ++J) rh[J] = fma(-u0[J], xk, rh[J]);
-#pragma unroll
-  for (int J = 0; J < NJ; ++J) {
-    u0[J] = u1[J];
-    u1[J] = u2[J];
-    if constexpr (K >= 3) u2[J] = nx[J];
-  }
-}
-
-template <int NM, int... I>
-__device__ __forceinline__ void lu2d_backsub(std::integer_sequence<int, I...>,
-                                             const double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB],
-                                             double (&rh)[Lu2d<NM>::NJ], double rpv, int ln, double& x) {
-  constexpr int NJ = Lu2d<NM>::NJ;
-  double u0[NJ], u1[NJ], u2[NJ];
-  lu2d_ucol<NM, NM - 1>(acc, ln, u0);
-  if constexpr (NM >= 2) lu2d_ucol<NM, NM - 2>(acc, ln, u1);
-  if constexpr (NM >= 3) lu2d_ucol<NM, NM - 3>(acc, ln, u2);
-  (lu2d_backsub_step<NM, NM - 1 - I>(acc, rh, rpv, ln, x, u0, u1, u2), ...);
+  (lu2d_step<NM, K>(acc, rh, pv, __builtin_amdgcn_readlane(pk, K), ln, viol, rpv, bad, piv, rp, col), ...);
 }
 
 template <int NM>
@@ -209,34 +183,17 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk
     for (int c = 0; c < NCB; ++c) acc[J][c] = (q < NM && lr + 4 * c < NM) ? row[lr + 4 * c] : 0.0;
     rh[J] = q < NM ? row[NM] : 0.0;
   }
-  uint32_t viol = 0;
+  uint64_t viol = 0;
   double rpv = 0.0;
   bool bad = false;
   lu2d_steps<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, pv, pk, ln, viol, rpv, bad);
-  // a non-finite U entry or reduced rhs: the +0-multiplier updates of the pivot half may
-  // have turned an entry the searched LU keeps into NaN — let the searched LU decide
-  // (checked before U overwrites Srow, so a false return leaves [S | rr] there)
-  bool fin = true;
+  if (bad || viol != 0) return false;
+  // x_k = b_k · (1 / u_kk): lane k = (lr, lc) holds position lc + 16·lr = k in rh[lr]
+  double r = rh[0];
 #pragma unroll
-  for (int J = 0; J < NJ; ++J) {
-    const int q = lc + 16 * J;
-#pragma unroll
-    for (int c = 0; c < NCB; ++c) {
-      const int col = lr + 4 * c;
-      if (q < NM && col < NM && col >= q) fin = fin & __builtin_isfinite(acc[J][c]);
-    }
-    if (q < NM) fin = fin & __builtin_isfinite(rh[J]);
-  }
-  if (bad || ballot((viol != 0) | !fin)) return false;
-  // Back substitution in the 2-D layout (oracle lu_solve_x: x_k = b_k · (1 / u_kk), then
-  // b_q ← fma(−u_qk, x_k, b_q) for the positions q < k, k descending).  rh is replicated
-  // over the four DPP rows and every lane takes the same fma with column k of U, which
-  // ds_bpermute hands it from DPP row Qk (U is final: fetched two steps ahead, off the
-  // chain); positions ≥ k are solved already, so their (dead) rh may take the fma too.
-  // The chain per step is a readlane, a product and an fma; U never goes to LDS.
-  double x = 0.0;
-  lu2d_backsub<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, rpv, ln, x);
-  dz = x;  // x_k = δ of column k: lane k holds unknown k
+  for (int J = 1; J < NJ; ++J)
+    if (lr == J) r = rh[J];
+  dz = r * rpv;
   return true;
 }
 
@@ -303,25 +260,25 @@ __device__ __forceinline__ int pivot_search(double ak, uint64_t rem, int ln) {
   return lowest_lane(ballot(khi == mhi && klo == mlo));
 }
 
-// Pivot k from its column (this lane's entry ak): the multipliers a_ik / piv and the
-// pivot row (−1: a zero pivot, the failed solve of src/solver.jl:84-88) into the LDS
-// buffers of parity k.
+// Pivot k from its column (this lane's entry ak): the multipliers a_ik · (1 / piv), −0 for
+// the pivot row (Gauss-Jordan: it takes fma(+0, u, a)), and the pivot row (−1: a zero pivot,
+// the failed solve of src/solver.jl:84-88) into the LDS buffers of parity k.
 __device__ __forceinline__ void publish_pivot(int k, double ak, uint64_t rem, int ln, double* Lb, int* Pb) {
   const int p = pivot_search(ak, rem, ln);
   const double piv = bcast(ak, p);
-  Lb[(k & 1) * 64 + ln] = ak * rcp_uniform(piv);  // oracle lu_solve_x, rcp
+  Lb[(k & 1) * 64 + ln] = (ln == p) ? -0.0 : ak * rcp_uniform(piv);  // oracle lu_solve_x, rcp = 2
   if (ln == 0) Pb[k & 1] = (piv == 0.0) ? -1 : p;
 }
 
-// LU with partial pivoting of [S | rhs] (row i at Srow[i·LDR], rhs in column NC) on W waves,
-// then the solve: the oracle's lu_solve operation for operation (bit-identical).  Wave w
-// owns columns [w·CW, (w+1)·CW) of every row (lane i = row i), the last wave also the
+// Gauss-Jordan with partial pivoting of [S | rhs] (row i at Srow[i·LDR], rhs in column NC)
+// on W waves: the oracle's lu_solve_x (rcp = 2) operation for operation (bit-identical).
+// Wave w owns columns [w·CW, (w+1)·CW) of every row (lane i = row i), the last wave also the
 // right-hand side.  Per pivot the owner of the pivot column searches it and publishes the
 // multipliers and the pivot row through LDS (double-buffered: one barrier per pivot); every
-// wave then updates its columns with the pivot row broadcast from lane p.  The owner of
-// column k+1 updates that column first and publishes pivot k+1 before its other columns, so
-// the pivot chain runs ahead of the bulk of the update.  The U rows go back to LDS and
-// wave 0 runs the back substitution.  dz: the solution entry of row `ln` on wave 0.
+// wave then updates its columns of every row with the pivot row broadcast from lane p.  The
+// owner of column k+1 updates that column first and publishes pivot k+1 before its other
+// columns, so the pivot chain runs ahead of the bulk of the update.  Then x_k = b_p / u_pk
+// (reciprocal) in lane p, handed to lane k.  dz: the solution entry of row `ln` on wave 0.
 template <int NC, int W, int NMAX>
 __device__ __forceinline__ bool lu_solve_mw(double* Srow, int LDR, double* Lb, int* Pb, int* pv, int wv, int ln,
                                             double& dz) {
@@ -346,13 +303,14 @@ __device__ __forceinline__ bool lu_solve_mw(double* Srow, int LDR, double* Lb, i
     const double l = Lb[(k & 1) * 64 + ln];
     rem &= ~(1ull << p);
     if (ln == p) my_step = k;
-    if (wv == 0 && ln == 0) pv[k] = p;
-    const bool upd = (rem >> ln) & 1ull;
+    // Gauss-Jordan: every row, the pivot row with multiplier −0, in uniform control flow (lanes
+    // ≥ NC hold zeros with a zero multiplier; an EXEC-narrowed update would put the broadcast
+    // groups below inside a divergent region, tools/check_dpp_hazards.py)
     const int wn = (k + 1) / CW, cn = (k + 1) % CW;  // owner of the next pivot column (static after unrolling)
     const bool next_owner = k + 1 < NC && wv == wn;
     if (next_owner) {
       const double u = bcast(acol[cn], p);
-      if (upd) acol[cn] = fma(-l, u, acol[cn]);
+      acol[cn] = fma(-l, u, acol[cn]);
       publish_pivot(k + 1, acol[cn], rem, ln, Lb, Pb);
     }
     double u[16];
@@ -361,32 +319,27 @@ __device__ __forceinline__ bool lu_solve_mw(double* Srow, int LDR, double* Lb, i
     for (int c = 0; c <= CW; ++c) {
       const int j = c < CW ? wv * CW + c : NC;  // the rhs slot: column NC of the last wave
       const bool live = (c < CW ? (j > k && j < NC && !(next_owner && c == cn)) : rhs_wave);
-      if (upd && live) acol[c] = fma(-l, u[c], acol[c]);
+      if (live) acol[c] = fma(-l, u[c], acol[c]);
     }
   }
-  // U and the reduced right-hand side back to LDS; wave 0 substitutes backwards
+  // row i was the pivot row of step my_step: x_{my_step} = b_i · (1 / u_{i, my_step}) in lane i
+  // (u from the wave owning column my_step, b from the rhs wave; the multiplier buffers are
+  // free once every wave is past the last step), then to lane my_step
+  __syncthreads();
 #pragma unroll
   for (int c = 0; c < CW; ++c) {
     const int j = wv * CW + c;
-    if (ln < NC && j < NC) Srow[ln * LDR + j] = acol[c];
+    if (ln < NC && j < NC && j == my_step) Lb[ln] = acol[c];
   }
-  if (rhs_wave && ln < NC) Srow[ln * LDR + NC] = acol[CW];
+  if (rhs_wave && ln < NC) Lb[64 + ln] = acol[CW];
+  if (wv == 0 && ln < NC) pv[my_step] = ln;
   __syncthreads();
   if (wv == 0) {
-    double a[NMAX];
-#pragma unroll
-    for (int j = 0; j < NMAX; ++j) a[j] = (ln < NC && j < NC) ? Srow[ln * LDR + j] : 0.0;
-    double b = ln < NC ? Srow[ln * LDR + NC] : 0.0;
-    dz = 0.0;
-#pragma clang loop unroll(full)
-    for (int k = NMAX - 1; k >= 0; --k) {
-      if (k < NC) {
-        const int p = __builtin_amdgcn_readfirstlane(pv[k]);
-        const double xk = bcast(b, p) * rcp_uniform(bcast(a[k], p));  // b_p · (1 / u_kk)
-        if (ln == k) dz = xk;
-        if (my_step < k) b = fma(-a[k], xk, b);
-      }
-    }
+    const double xi = ln < NC ? Lb[64 + ln] * (1.0 / Lb[ln]) : 0.0;
+    const int p = ln < NC ? pv[ln] : 0;
+    const int lo = __builtin_amdgcn_ds_bpermute(p << 2, __double2loint(xi));
+    const int hi = __builtin_amdgcn_ds_bpermute(p << 2, __double2hiint(xi));
+    dz = ln < NC ? __hiloint2double(hi, lo) : 0.0;
   }
   return true;
 }

@@ -82,7 +82,7 @@ class OracleNL(C.Structure):
     """oracle_nl of ipm_oracle.c: the generated init/eval of one nonlinear MCP."""
 
     _fields_ = [("init", C.c_void_p), ("eval", C.c_void_p), ("p", C.c_int32), ("has_s", C.c_int32),
-                ("size", C.c_int32), ("pad_", C.c_int32), ("qk_ptr", C.c_void_p), ("qk_idx", C.c_void_p),
+                ("size", C.c_int32), ("wave_schur", C.c_int32), ("qk_ptr", C.c_void_p), ("qk_idx", C.c_void_p),
                 ("rj_ptr", C.c_void_p), ("rj_idx", C.c_void_p), ("eval_theta", C.c_void_p),
                 ("tc_ptr", C.c_void_p), ("tc_idx", C.c_void_p), ("tr_ptr", C.c_void_p), ("tr_idx", C.c_void_p)]
 
@@ -130,7 +130,8 @@ def _nl_spec(nl) -> OracleNL:
     G.oracle_nl_table.argtypes = [C.c_int]
     fn = lambda f: C.cast(f, C.c_void_p).value
     t = [G.oracle_nl_table(w) for w in range(8)]
-    return OracleNL(fn(G.oracle_nl_init), fn(G.oracle_nl_eval), nl.p, int(nl.has_s), nl.size, 0, *t[:4],
+    return OracleNL(fn(G.oracle_nl_init), fn(G.oracle_nl_eval), nl.p, int(nl.has_s), nl.size,
+                    int(nl.solvers()["schur"]), *t[:4],
                     fn(G.oracle_nl_eval_theta), *t[4:])
 
 

@@ -88,7 +88,11 @@ typedef struct oracle_tables {
 typedef struct oracle_nl {
   void (*init)(const double* th, double* blk);
   void (*eval)(const double* th, const double* z, double* blk);
-  int32_t p, has_s, size, pad_;
+  int32_t p, has_s, size;
+  /* the module has the one-wave SCHUR kernel (codegen.py NLSystem.solvers()["schur"]): with
+   * linear_solver = SCHUR and kernel != MCPX_KERNEL_WORKGROUP the product solves S by the
+   * one-wave Gauss-Jordan (lu_solve_x rcp = 2), else by the workgroup kernels' LU (rcp = 1) */
+  int32_t wave_schur;
   /* structural nonzeros (mcp_amd/codegen.py NLSystem.structure): K(i) of row i of
    * Q = ∂G/∂y and J(k) of row k of R = ∂H/∂x, CSR with ascending indices */
   const int32_t *qk_ptr, *qk_idx, *rj_ptr, *rj_idx;
@@ -225,9 +229,17 @@ static double family_row(int family, int n, int m, const double* th, const doubl
 }
 
 /* ---- dense LU with partial pivoting on [J | b]; returns 0 ok, 1 singular ---- */
-/* rcp = 1 (the SCHUR step of generated nonlinear modules): multipliers a_ik · (1 / piv) and
- * back substitution x_k = b_p · (1 / u_kk), one correctly rounded reciprocal per pivot — the
- * arithmetic of the kernels' 2-D Gauss elimination (csrc/ipm_nl_kernel.hpp, lu2d_solve). */
+/* rcp = 1 (the SCHUR step of generated nonlinear modules on the workgroup-per-instance
+ * kernels): multipliers a_ik · (1 / piv) and back substitution x_k = b_p · (1 / u_kk), one
+ * correctly rounded reciprocal per pivot (csrc/ipm_wg_impl.hpp, lu_vr.hpp).
+ * rcp = 2 (the same step on the one-wave kernels, csrc/ipm_nl_kernel.hpp): Gauss-Jordan with
+ * the same partial pivoting — the pivot of column k is searched over the remaining rows as
+ * above, so the pivot sequence is the LU's — but every other row, pivoted before or not,
+ * takes the update a_ij ← fma(−l_i, u_j, a_ij) for j > k and the rhs (l_i = a_ik · (1 / piv)),
+ * and the pivot row itself takes it with multiplier +0 (a_pj ← fma(a_pj, +0, a_pj): the
+ * identity unless non-finite; the GPU updates its lanes uniformly); then x_k = b_p · (1 / u_pk)
+ * with no back substitution (the 40-step dependent chain it replaces was a third of a
+ * lone wave's Newton step on the lane-change game). */
 static int lu_solve_x(int N, double* J /* N×N row-major, destroyed */, double* b /* destroyed */,
                       double* dz, int* remaining, int* step_of, int* prow, int rcp) {
   for (int i = 0; i < N; ++i) remaining[i] = 1;
@@ -247,15 +259,26 @@ static int lu_solve_x(int N, double* J /* N×N row-major, destroyed */, double* 
     remaining[best] = 0;
     step_of[best] = k;
     prow[k] = best;
-    const double* u = J + (size_t)best * N;
+    double* u = J + (size_t)best * N;
     const double rp = 1.0 / piv;
     for (int i = 0; i < N; ++i) {
-      if (!remaining[i]) continue;
+      if (rcp == 2 ? i == best : !remaining[i]) continue;
       double* a = J + (size_t)i * N;
       const double l = rcp ? a[k] * rp : a[k] / piv;
       for (int j = k + 1; j < N; ++j) a[j] = fma(-l, u[j], a[j]);
       b[i] = fma(-l, b[best], b[i]);
     }
+    if (rcp == 2) { /* the pivot row, multiplier +0 */
+      for (int j = k + 1; j < N; ++j) u[j] = fma(u[j], 0.0, u[j]);
+      b[best] = fma(b[best], 0.0, b[best]);
+    }
+  }
+  if (rcp == 2) {
+    for (int k = 0; k < N; ++k) {
+      const int p = prow[k];
+      dz[k] = b[p] * (1.0 / J[(size_t)p * N + k]);
+    }
+    return 0;
   }
   for (int k = N - 1; k >= 0; --k) {
     const int p = prow[k];
@@ -459,7 +482,9 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           memcpy(w->bs, w->b, sizeof(double) * n);
           spd_ok = gj_spd_solve(n, w->Js, w->bs, w->dz) == 0;
         }
-        if (!spd_ok && lu_solve_x(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow, nl != NULL)) {
+        /* generated modules: Gauss-Jordan on the one-wave kernels, LU on the workgroup ones */
+        const int xmode = !nl ? 0 : ((nl->wave_schur && p->kernel != MCPX_KERNEL_WORKGROUP) ? 2 : 1);
+        if (!spd_ok && lu_solve_x(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow, xmode)) {
           status = MCPX_STATUS_FAILED;
           reason |= MCPX_FAIL_LINSOLVE;
           break;

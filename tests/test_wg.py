@@ -172,7 +172,10 @@ def test_lane_change_t2_forced_workgroup(gpu, oracle_lib, ls):
     mcp = game.mcp
     th = game.generate_random_parameter(np.random.default_rng(11), 48)
     tp, x0 = mcp.theta_map(th), game.initial_guess(th)
-    ref = oracle_lib.solve_batch_nl(mcp.nl, tp, x0=x0, linear_solver=ls, trace_len=TRACE, nthreads=8)
+    # the oracle follows the kernel: SCHUR solves S by LU on the workgroup kernels (by Gauss-Jordan
+    # on the one-wave ones, oracle lu_solve_x rcp = 2)
+    ref = oracle_lib.solve_batch_nl(mcp.nl, tp, x0=x0, linear_solver=ls, trace_len=TRACE, nthreads=8,
+                                    kernel="workgroup")
     got = solve_batch(_abi.FAMILY_NONLINEAR, mcp.nl.n, mcp.nl.m, tp, x0=x0, linear_solver=ls, trace_len=TRACE,
                       kernel="workgroup", module=mcp.module())
     assert_bit_exact(got, ref)

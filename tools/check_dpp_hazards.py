@@ -189,6 +189,18 @@ def narrowed_exec_hazards(insts, want: str):
             if not asm:
                 if o in ("s_branch", "s_setpc_b64", "s_endpgm"):
                     break  # not a fall-through predecessor
+                wm = re.fullmatch(r"s_mov_b64\s+exec,\s*(s\[\d+:\d+\])", tt)
+                if wm:  # the restore of a whole-wave-mode region (SGPR spills to VGPR lanes):
+                    # `s_or_saveexec_b64 sX, -1` … `s_mov_b64 exec, sX` leaves EXEC as it was
+                    w = j - 1
+                    while w >= 0 and insts[w][0] == k and not insts[w][3]:
+                        if re.search(r"\bexec\b", insts[w][1].split(",", 1)[0]) or insts[w][1].startswith("s_or_saveexec"):
+                            break
+                        w -= 1
+                    if (w >= 0 and insts[w][0] == k and not insts[w][3]
+                            and re.fullmatch(r"s_or_saveexec_b64\s+" + re.escape(wm.group(1)) + r",\s*-1", insts[w][1])):
+                        j = w - 1
+                        continue
                 if o in NARROW or (o in EXEC_WRITES and re.match(r"\S+\s+exec,", tt) and o != "s_or_b64"
                                    and not (o == "s_mov_b64" and "exec, -1" in tt)):
                     bad.append(f"NARROWED-EXEC BROADCAST in {k}: the asm block at instruction {i} switches EXEC "
