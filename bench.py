@@ -409,7 +409,7 @@ def main_lane_change(a, world, rank, local, dist, pl):
     import torch
 
     from mcp_amd import _abi
-    from mcp_amd.batch import alloc_device_outputs, solve_batch_device
+    from mcp_amd.batch import alloc_device_outputs, solve_batch_device, vjp_batch_device
     from mcp_amd.lane_change import LaneChangeGame
     from mcp_amd.qp_benchmark import chunked_slice
 
@@ -426,6 +426,14 @@ def main_lane_change(a, world, rank, local, dist, pl):
     stream = torch.cuda.current_stream(dev)
     ls = mcp.nl.default_solver()
 
+    # --sens: the application's solve + gradient (examples/utils.jl:236-261): Zygote's gradient of
+    # x₁ of the game solution w.r.t. θ, i.e. the rrule pullback of the cotangent e₁ on x
+    # (src/AutoDiff.jl:42-82) at each game's returned iterate, by mcpx_vjp_batch_module_device
+    gx = torch.zeros(B, n, dtype=torch.float64, device=dev)
+    gx[:, 0] = 1.0
+    dth = torch.empty(B, mcp.nl.p, dtype=torch.float64, device=dev)
+    vst = torch.empty(B, dtype=torch.int32, device=dev)
+
     def step(evs):
         if evs:
             evs[0][0].record(stream)
@@ -433,9 +441,17 @@ def main_lane_change(a, world, rank, local, dist, pl):
                            module=module, kernel=a.kernel)
         if evs:
             evs[0][1].record(stream)
+        if a.sens:
+            if evs:
+                evs[1][0].record(stream)
+            vjp_batch_device(_abi.FAMILY_NONLINEAR, n, m, theta, out["x"], out["y"], out["s"], gx, None, None,
+                             dtheta=dth, status=vst, stream=stream, module=module)
+            if evs:
+                evs[1][1].record(stream)
 
-    elapsed, ms = timed_steps(step, a, stream, world, dist, dev)
+    elapsed, ms = timed_steps(step, a, stream, world, dist, dev, 2 if a.sens else 1)
     kern_ms = float(np.mean(ms[0]))
+    vjp_ms = float(np.mean(ms[1])) if a.sens else 0.0
     step_s = [t * 1e-3 for t in ms[0]]
     newton = out["newton_iters"].to(torch.float64).sum().item()
     solved = (out["status"] == 0).to(torch.float64).sum().item()
@@ -445,9 +461,9 @@ def main_lane_change(a, world, rank, local, dist, pl):
         return
     # the generated module's content hash (its kernel headers included) keys the evidence too:
     # the nonlinear kernels live in the module, not in libmcpx.so
-    cfg = {"mode": "c4", "horizon": a.lane_change, "batch_per_gpu": B, "linear_solver": ls,
+    cfg = {"mode": "c4s" if a.sens else "c4", "horizon": a.lane_change, "batch_per_gpu": B, "linear_solver": ls,
            "module": mcp.nl.module_key(), "kernel": a.kernel}
-    key = f"c4_lane_t{a.lane_change}_b{B}"
+    key = f"c4{'s' if a.sens else ''}_lane_t{a.lane_change}_b{B}"
     ev = evidence(key, cfg)
     mw = ls == "schur" and a.kernel == "multiwave" and module.has_schur_mw
     kernel = "mcpx_nl_solve_" + ls + ("_mw" if mw else ("" if mcp.nl.solvers()[ls] and a.kernel != "workgroup"
@@ -460,7 +476,9 @@ def main_lane_change(a, world, rank, local, dist, pl):
                   "nonzeros" if ls == "schur" else "") + "); bound: per-wave latency (PMC: waves stall on LDS/VALU "
                   "dependencies, DESIGN.md §4)")
     res = {
-        "metric": "MCP solves/sec (lane-change trajectory game, generated nonlinear module)",
+        "metric": ("MCP solve+VJP/sec (lane-change trajectory game, generated nonlinear module, rrule pullback of "
+                   "x₁ as examples/utils.jl:236-261)" if a.sens else
+                   "MCP solves/sec (lane-change trajectory game, generated nonlinear module)"),
         "value": a.steps * pl["global_batch"] / elapsed, "unit": "solves/s", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
         "scaling": pl["scaling"], "vs_baseline": None, "dtype": "f64",
@@ -475,6 +493,11 @@ def main_lane_change(a, world, rank, local, dist, pl):
         "summary_statistics": summary_statistics(step_s, B, solved_all / pl["global_batch"]),
         "evidence": evidence_id(key, cfg),
     }
+    if a.sens:
+        res["solve_kernel_ms"] = kern_ms
+        res["vjp_kernel_ms"] = vjp_ms
+        res["vjp_kernel"] = "mcpx_nl_vjp_wg"
+        res["vjp_status_nonzero"] = int((vst != 0).sum().item())
     if world == 1 and a.cpu_sample != 0:
         from oracle import coracle
 
@@ -489,6 +512,14 @@ def main_lane_change(a, world, rank, local, dist, pl):
         got = {f: out[f][:k].cpu().numpy() for f in C4_FIELDS}
         res["parity"] = parity_report(got, r, C4_FIELDS, k, "oracle/ipm_oracle.c with the same generated G/H "
                                       "code (cpu_baseline sample)")
+        if a.sens:  # the pullback of the same games against oracle_vjp_batch_nl at the GPU's solutions
+            x, y, s_ = (out[f][:k].cpu().numpy() for f in ("x", "y", "s"))
+            gxh = np.zeros((k, n))
+            gxh[:, 0] = 1.0
+            rd, rs = coracle.vjp_batch_nl(mcp.nl, theta_host[:k], x, y, s_, gxh, None, None, nthreads=th)
+            res["vjp_parity"] = parity_report({"dtheta": dth[:k].cpu().numpy(), "status": vst[:k].cpu().numpy()},
+                                              {"dtheta": rd, "status": rs}, ("dtheta", "status"), k,
+                                              "oracle_vjp_batch_nl on the GPU's solutions")
         res["cpu_baseline"] = cb
     print(json.dumps(res), flush=True)
 

@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "ipm_kernel.h"
 
 // A DPP read of a VGPR needs 2 wait states after a VALU write of it, and hipcc
@@ -863,6 +865,146 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
   return true;
 }
 
+// The same Gauss-Jordan with compile-time dimension NN and one step of lookahead (the fast
+// pass of the compile-time-(n, m) SCHUR kernels, MCPX_GJ_LOOKAHEAD).  Step K updates the local
+// column block holding column K + 1 first (every half, the pivot half last), then reads pivot
+// K + 1, starts its reciprocal and fetches its column by ds_bpermute, and only then updates
+// the other blocks, so the reciprocal's dependent chain and the LDS latency of the column
+// run beside the bulk of step K's fmas instead of heading step K + 1.  Every entry takes the
+// same fma in the same order as gj2d_spd.  The reciprocal is the branch-free fast form, and
+// the pivots are checked once at the end: a pivot ≤ 0 or outside the fast reciprocal's exact
+// range (|piv| ∉ [2⁻⁵⁰⁰, 2⁵⁰⁰]) makes the caller (pass 1) defer the instance to the second
+// pass, which takes the exact rcp_uniform of gj2d_spd — so the bits stay the oracle's.  Per
+// pivot the bookkeeping is 2 readlanes, the 7-instruction reciprocal, one product per half and
+// the pivot-row zeroing by a constant lane mask (2 v_cndmask); the pivot itself goes to LDS
+// by a one-lane ds_write (no VALU), where the final division reads it.
+#ifndef MCPX_GJ_LOOKAHEAD
+#define MCPX_GJ_LOOKAHEAD 1
+#endif
+typedef __attribute__((address_space(3))) double lds_f64;
+
+// The pivot of step K, the entry `v` holds in lane LANE, to LDS slot K of `base` by a one-lane
+// ds_write under a constant EXEC mask (no VALU; the Gauss-Jordan's final division reads it).
+template <int K, int LANE>
+__device__ __forceinline__ void record_pivot(uint32_t base, double v) {
+  uint64_t save;
+  asm volatile("s_mov_b64 %0, exec\n s_mov_b64 exec, %3\n ds_write_b64 %1, %2 offset:%4\n s_mov_b64 exec, %0"
+               : "=&s"(save) : "v"(base), "v"(v), "s"(1ull << LANE), "n"(8 * K) : "memory");
+}
+
+// v with the lanes of `mask` (an SGPR constant) replaced by +0: two v_cndmask_b32, no compare.
+__device__ __forceinline__ double zero_lanes(double v, uint64_t mask) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  asm volatile("v_cndmask_b32_e64 %0, %0, 0, %2\n v_cndmask_b32_e64 %1, %1, 0, %2" : "+v"(lo), "+v"(hi) : "s"(mask));
+  return __hiloint2double(hi, lo);
+}
+
+template <int NT, int NN, int K>
+__device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&rh)[NT], int ln, uint32_t pbase,
+                                             double& piv, double& rp, double (&col)[NT]) {
+  constexpr int Jk = K >> 4, Rk = K & 15;
+  constexpr bool NX = K + 1 < NN;
+  constexpr int K1 = NX ? K + 1 : K;
+  constexpr int Jn = K1 >> 4, Rn = K1 & 15, Qn = K1 & 3, Cn = K1 >> 2, In = Cn >> 2, rn = Cn & 3;
+  __builtin_amdgcn_sched_barrier(0);  // one step at a time
+  const int lc = ln & 15;
+  double nl[NT];
+#pragma unroll
+  for (int J = 0; J < NT; ++J) nl[J] = (-col[J]) * rp;
+  nl[Jk] = zero_lanes(nl[Jk], 0x0001000100010001ull << Rk);  // the pivot row (lc = Rk): multiplier +0
+  if constexpr (NX) {
+    if (4 * Cn + 3 > K) {  // the block of column K + 1 (always live at step K)
+#pragma unroll
+      for (int J = 0; J < NT; ++J) {
+        if (J == Jk) continue;
+        switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast<R, false>(acc[In][J][rn], acc[In][Jk][rn], nl[J]); break;
+          MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+          MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14)
+          MCPX_CASE(15)
+#undef MCPX_CASE
+        }
+      }
+      switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast_self<R, false>(acc[In][Jk][rn], nl[Jk]); break;
+        MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+        MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14)
+        MCPX_CASE(15)
+#undef MCPX_CASE
+      }
+    }
+#pragma unroll
+    for (int J = 0; J < NT; ++J) col[J] = bperm_f64_addr(acc[In][J][rn], (16 * Qn + lc) << 2);
+    piv = bcast(acc[In][Jn][rn], 16 * Qn + Rn);
+    record_pivot<K1, 16 * Qn + Rn>(pbase, acc[In][Jn][rn]);
+    rp = rcp_fast(piv);
+  }
+#pragma unroll
+  for (int J = 0; J < NT; ++J) {
+    if (J == Jk) continue;  // the pivot half last
+#pragma unroll
+    for (int c = 0; c < 4 * NT; ++c) {
+      if (4 * c + 3 <= K || (NX && c == Cn)) continue;
+      switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast<R, false>(acc[c >> 2][J][c & 3], acc[c >> 2][Jk][c & 3], nl[J]); break;
+        MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+        MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14)
+        MCPX_CASE(15)
+#undef MCPX_CASE
+      }
+    }
+    switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast<R, false>(rh[J], rh[Jk], nl[J]); break;
+      MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+      MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14) MCPX_CASE(15)
+#undef MCPX_CASE
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4 * NT; ++c) {
+    if (4 * c + 3 <= K || (NX && c == Cn)) continue;
+    switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast_self<R, false>(acc[c >> 2][Jk][c & 3], nl[Jk]); break;
+      MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+      MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14) MCPX_CASE(15)
+#undef MCPX_CASE
+    }
+  }
+  switch (Rk) {
+#define MCPX_CASE(R) case R: fmac_row_bcast_self<R, false>(rh[Jk], nl[Jk]); break;
+    MCPX_CASE(0) MCPX_CASE(1) MCPX_CASE(2) MCPX_CASE(3) MCPX_CASE(4) MCPX_CASE(5) MCPX_CASE(6) MCPX_CASE(7)
+    MCPX_CASE(8) MCPX_CASE(9) MCPX_CASE(10) MCPX_CASE(11) MCPX_CASE(12) MCPX_CASE(13) MCPX_CASE(14) MCPX_CASE(15)
+#undef MCPX_CASE
+  }
+}
+
+template <int NT, int NN, int... K>
+__device__ __forceinline__ bool gj2d_spd_la(std::integer_sequence<int, K...>, double (&acc)[NT][NT][4],
+                                            double (&rh)[NT], int ln, double& xo) {
+  __shared__ double spiv[NN];  // pivot k in slot k (record_pivot)
+  const uint32_t pbase = (uint32_t)(uintptr_t)(lds_f64*)spiv;
+  const int lc = ln & 15;
+  double col[NT];
+  double piv = bcast(acc[0][0][0], 0);  // pivot 0: column 0 = tile 0, element 0, DPP row 0
+  record_pivot<0, 0>(pbase, acc[0][0][0]);
+  double rp = rcp_fast(piv);
+#pragma unroll
+  for (int J = 0; J < NT; ++J) col[J] = bperm_f64_addr(acc[0][J][0], lc << 2);
+  (gj2d_la_step<NT, NN, K>(acc, rh, ln, pbase, piv, rp, col), ...);
+  // every pivot > 0 and inside the fast reciprocal's exact range, checked once at the end
+  // (a bad pivot only made the later steps compute discarded values); lane i reads pivot i
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the one-lane ds_writes of the steps
+  __builtin_amdgcn_wave_barrier();
+  const double d = spiv[ln < NN ? ln : 0];
+  if (ballot((ln < NN) & !((d > 0.0) & rcp_fast_ok(d)))) return false;
+  double r = rh[0];
+#pragma unroll
+  for (int J = 1; J < NT; ++J)
+    if ((ln >> 4) == J) r = rh[J];
+  xo = r / d;
+  return true;
+}
+
 // The rrule pullback fused into the solve kernel's epilogue (defined in
 // sens_kernel_impl.hpp; only the FUSE instantiations of ipm_inst_fused.hip use it).
 template <int NV, int FAMILY, int NT, bool LU>
@@ -1084,7 +1226,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
           for (int J = 0; J < NT; ++J) rh2[J] = (16 * J + (ln & 15) < n) ? sB[16 * J + (ln & 15)] : 0.0;
           // lane 16J + lc owns row 16J + lc.  Opaque dimension: with a constant one the
           // scheduler merges the 32 steps (+5 % VALU in the fast pass)
-          ok = gj2d_spd<NT, (NC == 0)>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, dz);
+          if constexpr (PASS == 1 && NC > 0 && MCPX_GJ_LOOKAHEAD)
+            ok = gj2d_spd_la<NT, NC>(std::make_integer_sequence<int, NC>{}, acc, rh2, ln, dz);
+          else
+            ok = gj2d_spd<NT, (NC == 0)>(acc, rh2, (NC > 0) ? opaque(NS) : NS, ln, dz);
         }
         if constexpr (PASS == 1) {
           if (!ok) {  // S not numerically SPD at this step: second pass

@@ -12,7 +12,7 @@ T, B = int(sys.argv[1]), int(sys.argv[2])
 g = LaneChangeGame(T)
 mcp = g.mcp
 th = np.ascontiguousarray(mcp.theta_map(chunked_slice(lambda rng, k: g.generate_random_parameter(rng, k), 1, 0, B)))
-out = os.path.join(ROOT, "tools", "ubench_data")
+out = os.path.join(ROOT, "tools", "phase_data")  # shipped to the box (ubench_data is not)
 os.makedirs(out, exist_ok=True)
 th.tofile(os.path.join(out, f"theta_lane_t{T}_b{B}.bin"))
 mcp.nl.build_module()  # the product module (and its .hip text)
