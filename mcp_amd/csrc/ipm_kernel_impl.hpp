@@ -657,7 +657,9 @@ template <int NT>
 __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, const double* ta, int lda,
                                                  const double* sD, int ln, int n, int m, double tol,
                                                  d4 (&acc)[NT][NT]) {
-  const int lr = ln >> 4, lc = ln & 15;
+  // lr ∈ [0, 3] made visible to the compiler (ln is opaque_lane in the Newton loop): with
+  // compile-time (n, m) the range checks of the loads and masks below then fold away
+  const int lr = (ln >> 4) & 3, lc = ln & 15;
   {  // C = Mᵀ blocks: element (p = lr + 4r, q = lc) of tile (I, J) is M[16J+q][16I+p] = θ[(16I+p)·n + 16J+q]
     double mv[NT][NT][4];
 #pragma unroll
@@ -885,17 +887,23 @@ typedef __attribute__((address_space(3))) double lds_f64;
 
 // The pivot of step K, the entry `v` holds in lane LANE, to LDS slot K of `base` by a one-lane
 // ds_write under a constant EXEC mask (no VALU; the Gauss-Jordan's final division reads it).
+// (The lane masks pass through an opaque asm first: as plain "s" constants the compiler hoists
+// all 32 + 16 distinct masks out of the Newton loop and spills SGPRs.)
 template <int K, int LANE>
 __device__ __forceinline__ void record_pivot(uint32_t base, double v) {
-  uint64_t save;
+  uint64_t save, msk = 1ull << LANE;
+  asm volatile("" : "+s"(msk));
   asm volatile("s_mov_b64 %0, exec\n s_mov_b64 exec, %3\n ds_write_b64 %1, %2 offset:%4\n s_mov_b64 exec, %0"
-               : "=&s"(save) : "v"(base), "v"(v), "s"(1ull << LANE), "n"(8 * K) : "memory");
+               : "=&s"(save) : "v"(base), "v"(v), "s"(msk), "n"(8 * K) : "memory");
 }
 
-// v with the lanes of `mask` (an SGPR constant) replaced by +0: two v_cndmask_b32, no compare.
-__device__ __forceinline__ double zero_lanes(double v, uint64_t mask) {
+// v with the lanes lc = R of every DPP row replaced by +0: two v_cndmask_b32, no compare.
+template <int R>
+__device__ __forceinline__ double zero_lanes(double v) {
   int lo = __double2loint(v), hi = __double2hiint(v);
-  asm volatile("v_cndmask_b32_e64 %0, %0, 0, %2\n v_cndmask_b32_e64 %1, %1, 0, %2" : "+v"(lo), "+v"(hi) : "s"(mask));
+  uint64_t msk = 0x0001000100010001ull << R;
+  asm volatile("" : "+s"(msk));
+  asm volatile("v_cndmask_b32_e64 %0, %0, 0, %2\n v_cndmask_b32_e64 %1, %1, 0, %2" : "+v"(lo), "+v"(hi) : "s"(msk));
   return __hiloint2double(hi, lo);
 }
 
@@ -911,7 +919,7 @@ __device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&
   double nl[NT];
 #pragma unroll
   for (int J = 0; J < NT; ++J) nl[J] = (-col[J]) * rp;
-  nl[Jk] = zero_lanes(nl[Jk], 0x0001000100010001ull << Rk);  // the pivot row (lc = Rk): multiplier +0
+  nl[Jk] = zero_lanes<Rk>(nl[Jk]);  // the pivot row (lc = Rk): multiplier +0
   if constexpr (NX) {
     if (4 * Cn + 3 > K) {  // the block of column K + 1 (always live at step K)
 #pragma unroll
