@@ -73,7 +73,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 Z_VOLATILE_ABOVE = int(os.environ.get("MCPX_NL_Z_VOLATILE_ABOVE", "128"))
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
-GEN_VERSION = 6
+GEN_VERSION = 7
 EVAL_PARTS = 4  # mcpx_nl_eval_p0..p3: the generated eval split over the 4-wave SCHUR kernel
 _MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function",
                  "-mllvm", "-amdgpu-mfma-vgpr-form=1")
@@ -263,7 +263,7 @@ class NLSystem:
         raise NotImplementedError(f"nonlinear MCP with n={self.n}, m={self.m} exceeds every kernel's LDS budget")
 
     # ---- emission ------------------------------------------------------------
-    def _block(self, entries, with_z: bool, out: str = "blk") -> list:
+    def _block(self, entries, with_z: bool, out: str = "blk", cse_out: dict | None = None) -> list:
         """Straight-line C for `entries` after common-subexpression elimination.  Each
         CSE temporary is emitted right before the first statement that needs it
         (dependency order kept), not all at the top: at horizon T = 10 the
@@ -277,6 +277,8 @@ class NLSystem:
         if not entries:
             return []
         reps, red = sp.cse([e for _, e in entries], symbols=sp.numbered_symbols("c"), order="canonical")
+        if cse_out is not None:  # the same CSE for the lane-parallel eval (nl_vec)
+            cse_out.update(reps=reps, red=red, names=dict(names))
         pr = _Printer(names)
         rep_of = {sym: e for sym, e in reps}
         order = {sym: i for i, (sym, _) in enumerate(reps)}
@@ -399,7 +401,12 @@ class NLSystem:
 
     def _emit(self) -> str:
         init = self._block(self.const_entries, with_z=False)
-        ev = self._block(self.var_entries + self.residuals, with_z=True)
+        cse = {}
+        ev = self._block(self.var_entries + self.residuals, with_z=True, cse_out=cse)
+        from . import nl_vec
+
+        self.vec = (nl_vec.build(self, cse["reps"], cse["red"], self.var_entries + self.residuals, cse["names"])
+                    if cse else None)
         evt = self._block(self.theta_entries, with_z=True, out="dth")
         evp = self._block_parts(self.var_entries + self.residuals, True, EVAL_PARTS)
         parts = []
@@ -447,6 +454,7 @@ class NLSystem:
             arr("mcpx_nl_tc_idx", tci),
             arr("mcpx_nl_tr_ptr", trp),
             arr("mcpx_nl_tr_idx", tri),
+            *(nl_vec.emit(self.vec) if self.vec is not None else []),
             "MCPX_NL_FN void mcpx_nl_init(const double* MCPX_NL_RESTRICT th, double* MCPX_NL_RESTRICT blk) {",
             "  (void)th;",
             "  (void)blk;",

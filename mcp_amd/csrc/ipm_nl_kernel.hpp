@@ -344,6 +344,39 @@ __device__ __forceinline__ bool lu_solve_mw(double* Srow, int LDR, double* Lb, i
   return true;
 }
 
+// ---- lane-parallel eval (mcp_amd/nl_vec.py) ----------------------------------------------
+// The generated mcpx_nl_eval rewritten as chains acc = A₀·B₀ + A₁·B₁ + … (each product and
+// sum rounded once, the C text's operation order; exact, see nl_vec.py), one chain per lane
+// and slot, levels in order.  Operands and destinations are byte offsets into the wave's `ev`
+// LDS array (blk | z | θ | constants | temporaries | dummy): per lane and term one word
+// (A | B << 16), held in VGPRs for the whole solve.  One wave: LDS ops complete in order, so
+// no barrier between levels.
+#if defined(MCPX_NL_VEC)
+constexpr bool VEC = true;
+constexpr int kVecSteps[] = {MCPX_NL_VEC_STEPS};
+__device__ __forceinline__ double ev_at(const double* ev, uint32_t byte_off) {
+  return *(const double*)((const char*)ev + byte_off);
+}
+template <int S = 0, int W = 0>
+__device__ __forceinline__ void eval_vec(double* ev, const uint32_t (&w)[MCPX_NL_VEC_NWORD],
+                                         const uint32_t (&d)[MCPX_NL_VEC_NSLOT]) {
+  if constexpr (S < MCPX_NL_VEC_NSLOT) {
+    constexpr int K = kVecSteps[S];
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const uint32_t x = w[W + t];
+      const double prod = ev_at(ev, x & 0xffffu) * ev_at(ev, x >> 16);
+      acc = t == 0 ? prod : acc + prod;
+    }
+    *(double*)((char*)ev + d[S]) = acc;
+    eval_vec<S + 1, W + K>(ev, w, d);
+  }
+}
+#else
+constexpr bool VEC = false;
+#endif
+
 // MW = true (SCHUR only): one 4-wave workgroup per instance (mcpx_nl_solve_schur_mw).  The
 // LU runs on all four waves (lu_solve_mw); wave 0 does the rest, the other waves follow the
 // same control flow from the shared state in LDS (every branch below depends only on LDS
@@ -358,8 +391,23 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   static_assert(SCH || m <= 64, "REDUCED / DENSE hold every constraint in a lane");
   constexpr int BLK = imax(1, OFF_S + (SCH ? 0 : m * m));  // RED / DENSE read S (a zero block if absent)
   constexpr int NZ = imax(1, N), MZ = imax(1, m);
-  __shared__ double blk[BLK];
-  __shared__ double zs[NZ], dzs[NZ], Fs[NZ];
+  // the one-wave SCHUR kernel with a lane-parallel eval: blk and z inside its `ev` array
+  constexpr bool EV = VEC && SCH && !MW;
+#if defined(MCPX_NL_VEC)
+  static_assert(!EV || (MCPX_NL_VEC_OFF_Z >= BLK && MCPX_NL_VEC_OFF_T >= MCPX_NL_VEC_OFF_Z + NZ), "ev layout");
+  __shared__ double ev[EV ? MCPX_NL_VEC_EV : 1];
+  uint32_t vw[MCPX_NL_VEC_NWORD], vd[MCPX_NL_VEC_NSLOT];
+#else
+  __shared__ double ev[1];
+#endif
+  __shared__ double blk_own[EV ? 1 : BLK], zs_own[EV ? 1 : NZ];
+  double* const blk = EV ? ev : blk_own;
+#if defined(MCPX_NL_VEC)
+  double* const zs = EV ? ev + MCPX_NL_VEC_OFF_Z : zs_own;
+#else
+  double* const zs = zs_own;
+#endif
+  __shared__ double dzs[NZ], Fs[NZ];
   constexpr int LDR = n + 1;  // SCHUR: lane-private LDS rows of S (odd stride: 2-way bank conflicts at most)
   __shared__ double Srow[SCH ? imax(1, n * LDR) : 1];
   __shared__ double sRw[SCH ? MZ : 1], sDi[SCH ? MZ : 1], sRy[SCH ? MZ : 1], sTy[SCH ? MZ : 1];
@@ -388,6 +436,16 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
       zs[n + m + k] = args.s0 ? args.s0[inst * m + k] : 1.0;
     }
   }
+#if defined(MCPX_NL_VEC)
+  if constexpr (EV) {  // θ and the constants into ev, the lane's operand words into VGPRs
+    for (int k = lane; k < MCPX_NL_P; k += 64) ev[MCPX_NL_VEC_OFF_T + k] = th[k];
+    for (int k = lane; k < MCPX_NL_VEC_NC; k += 64) ev[MCPX_NL_VEC_OFF_C + k] = mcpx_nl_vec_const[k];
+#pragma unroll
+    for (int k = 0; k < MCPX_NL_VEC_NWORD; ++k) vw[k] = mcpx_nl_vec_word[k * 64 + lane];
+#pragma unroll
+    for (int k = 0; k < MCPX_NL_VEC_NSLOT; ++k) vd[k] = mcpx_nl_vec_dst[k * 64 + lane];
+  }
+#endif
   __syncthreads();
   if (tid == 0) mcpx_nl_init(th, blk);
 
@@ -417,8 +475,12 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
           else if (wv == 2) mcpx_nl_eval_p2(th, zs, blk);
           else mcpx_nl_eval_p3(th, zs, blk);
         }
-      } else if (tid == 0) {
-        mcpx_nl_eval(th, zs, blk);
+      } else {
+#if defined(MCPX_NL_VEC)
+        if constexpr (EV) eval_vec(ev, vw, vd);
+        else
+#endif
+        if (tid == 0) mcpx_nl_eval(th, zs, blk);
       }
 #else
       if (tid == 0) mcpx_nl_eval(th, zs, blk);

@@ -124,6 +124,44 @@ def test_generated_modules_compile(lane):
             assert (f"mcpx_nl_solve_{s}_wg\0".encode() in blob) == ok, s
 
 
+def test_lane_parallel_eval_matches_generated_c(lane, oracle_lib):
+    """The chain rewrite of mcpx_nl_eval (mcp_amd/nl_vec.py) that the one-wave SCHUR kernel
+    evaluates lane-parallel is bitwise the generated C text the oracle compiles: random z over
+    wide magnitudes with ±0, Inf and NaN entries, every output entry of blk compared by bits
+    (NaN = NaN whatever its payload, as in every parity test).
+    Transcendental modules keep the straight-line eval (no program)."""
+    import ctypes as C
+
+    from oracle import coracle
+
+    assert trig_mcp().nl.vec is None
+    rng = np.random.default_rng(7)
+    for mcp, theta_of in ((lane.mcp, lambda k: lane.mcp.theta_map(lane.generate_random_parameter(rng, k))),
+                          (cubic_mcp(), _cubic_theta)):
+        nl = mcp.nl
+        prog = nl.vec
+        assert prog is not None and prog.levels()
+        G = coracle.nl_lib(nl)
+        ev = G.oracle_nl_eval
+        ev.restype, ev.argtypes = None, [C.c_void_p] * 3
+        ini = G.oracle_nl_init
+        ini.restype, ini.argtypes = None, [C.c_void_p] * 2
+        ths = np.atleast_2d(theta_of(300))
+        for trial in range(300):
+            th = np.ascontiguousarray(ths[trial % len(ths)], dtype=np.float64)
+            z = rng.standard_normal(nl.n + 2 * nl.m) * 10.0 ** rng.integers(-6, 7)
+            sel = rng.integers(0, len(z), 3)
+            z[sel] = [0.0, -0.0, [np.inf, -np.inf, np.nan][trial % 3]] if trial % 5 == 0 else z[sel]
+            ref = np.zeros(nl.size + 1)
+            ini(th.ctypes.data, ref.ctypes.data)
+            got = ref[:nl.size].copy()
+            ev(th.ctypes.data, z.ctypes.data, ref.ctypes.data)
+            prog.emulate(th, z, got)
+            r = ref[:nl.size]
+            same_bits = got.view(np.uint64) == r.view(np.uint64)
+            assert (same_bits | (np.isnan(got) & np.isnan(r))).all(), trial  # NaN payloads aside
+
+
 # ---------------------------------------------------------------- GPU
 
 
