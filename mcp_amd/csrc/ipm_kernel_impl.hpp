@@ -877,26 +877,21 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
 // the pivots are checked once at the end: a pivot ≤ 0 or outside the fast reciprocal's exact
 // range (|piv| ∉ [2⁻⁵⁰⁰, 2⁵⁰⁰]) makes the caller (pass 1) defer the instance to the second
 // pass, which takes the exact rcp_uniform of gj2d_spd — so the bits stay the oracle's.  Per
-// pivot the bookkeeping is 2 readlanes, the 7-instruction reciprocal, one product per half and
-// the pivot-row zeroing by a constant lane mask (2 v_cndmask); the pivot itself goes to LDS
-// by a one-lane ds_write (no VALU), where the final division reads it.
+// pivot the bookkeeping is 2 readlanes, the 7-instruction reciprocal, one product per half, the
+// pivot-row zeroing by a constant lane mask (2 v_cndmask, no compare) and the pivot recorded in
+// its lane by 2 v_writelane for the final division.  (Recording it instead by a one-lane
+// ds_write under an EXEC switch, no VALU, gave wrong last bits on the GPU in every instance:
+// tools/parity_probe.py, profiles/r04; not kept.)
 #ifndef MCPX_GJ_LOOKAHEAD
 #define MCPX_GJ_LOOKAHEAD 1
 #endif
-typedef __attribute__((address_space(3))) double lds_f64;
-
+#ifndef MCPX_GJ_ZMASK
+#define MCPX_GJ_ZMASK 1
+#endif
 // The pivot of step K, the entry `v` holds in lane LANE, to LDS slot K of `base` by a one-lane
 // ds_write under a constant EXEC mask (no VALU; the Gauss-Jordan's final division reads it).
-// (The lane masks pass through an opaque asm first: as plain "s" constants the compiler hoists
-// all 32 + 16 distinct masks out of the Newton loop and spills SGPRs.)
-template <int K, int LANE>
-__device__ __forceinline__ void record_pivot(uint32_t base, double v) {
-  uint64_t save, msk = 1ull << LANE;
-  asm volatile("" : "+s"(msk));
-  asm volatile("s_mov_b64 %0, exec\n s_mov_b64 exec, %3\n ds_write_b64 %1, %2 offset:%4\n s_mov_b64 exec, %0"
-               : "=&s"(save) : "v"(base), "v"(v), "s"(msk), "n"(8 * K) : "memory");
-}
-
+// (The lane mask passes through an opaque asm first: as a plain "s" constant the compiler
+// hoists all 16 distinct masks out of the Newton loop and spills SGPRs.)
 // v with the lanes lc = R of every DPP row replaced by +0: two v_cndmask_b32, no compare.
 template <int R>
 __device__ __forceinline__ double zero_lanes(double v) {
@@ -908,8 +903,8 @@ __device__ __forceinline__ double zero_lanes(double v) {
 }
 
 template <int NT, int NN, int K>
-__device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&rh)[NT], int ln, uint32_t pbase,
-                                             double& piv, double& rp, double (&col)[NT]) {
+__device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&rh)[NT], int ln, double& piv,
+                                             double& rp, double (&col)[NT], double& dgl) {
   constexpr int Jk = K >> 4, Rk = K & 15;
   constexpr bool NX = K + 1 < NN;
   constexpr int K1 = NX ? K + 1 : K;
@@ -919,7 +914,8 @@ __device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&
   double nl[NT];
 #pragma unroll
   for (int J = 0; J < NT; ++J) nl[J] = (-col[J]) * rp;
-  nl[Jk] = zero_lanes<Rk>(nl[Jk]);  // the pivot row (lc = Rk): multiplier +0
+  if constexpr (MCPX_GJ_ZMASK) nl[Jk] = zero_lanes<Rk>(nl[Jk]);  // the pivot row (lc = Rk): multiplier +0
+  else if (lc == Rk) nl[Jk] = 0.0;
   if constexpr (NX) {
     if (4 * Cn + 3 > K) {  // the block of column K + 1 (always live at step K)
 #pragma unroll
@@ -944,7 +940,7 @@ __device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&
 #pragma unroll
     for (int J = 0; J < NT; ++J) col[J] = bperm_f64_addr(acc[In][J][rn], (16 * Qn + lc) << 2);
     piv = bcast(acc[In][Jn][rn], 16 * Qn + Rn);
-    record_pivot<K1, 16 * Qn + Rn>(pbase, acc[In][Jn][rn]);
+    dgl = writelane_f64(dgl, piv, K1);  // pivot K + 1 in lane K + 1 (the final division)
     rp = rcp_fast(piv);
   }
 #pragma unroll
@@ -989,21 +985,17 @@ __device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&
 template <int NT, int NN, int... K>
 __device__ __forceinline__ bool gj2d_spd_la(std::integer_sequence<int, K...>, double (&acc)[NT][NT][4],
                                             double (&rh)[NT], int ln, double& xo) {
-  __shared__ double spiv[NN];  // pivot k in slot k (record_pivot)
-  const uint32_t pbase = (uint32_t)(uintptr_t)(lds_f64*)spiv;
   const int lc = ln & 15;
   double col[NT];
   double piv = bcast(acc[0][0][0], 0);  // pivot 0: column 0 = tile 0, element 0, DPP row 0
-  record_pivot<0, 0>(pbase, acc[0][0][0]);
+  double dgl = writelane_f64(1.0, piv, 0);  // pivot k in lane k
   double rp = rcp_fast(piv);
 #pragma unroll
   for (int J = 0; J < NT; ++J) col[J] = bperm_f64_addr(acc[0][J][0], lc << 2);
-  (gj2d_la_step<NT, NN, K>(acc, rh, ln, pbase, piv, rp, col), ...);
+  (gj2d_la_step<NT, NN, K>(acc, rh, ln, piv, rp, col, dgl), ...);
   // every pivot > 0 and inside the fast reciprocal's exact range, checked once at the end
-  // (a bad pivot only made the later steps compute discarded values); lane i reads pivot i
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the one-lane ds_writes of the steps
-  __builtin_amdgcn_wave_barrier();
-  const double d = spiv[ln < NN ? ln : 0];
+  // (a bad pivot only made the later steps compute discarded values); lane i holds pivot i
+  const double d = dgl;
   if (ballot((ln < NN) & !((d > 0.0) & rcp_fast_ok(d)))) return false;
   double r = rh[0];
 #pragma unroll

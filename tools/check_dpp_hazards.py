@@ -22,6 +22,10 @@
    first is a hazard (the number of source registers redefined in between is
    reported).
 
+3. EXEC writes inside inline asm followed by a DPP instruction within 5 wait states (the
+   gfx9 table's EXEC-write → DPP distance, applied conservatively to SALU writes too, which
+   the compiler cannot pad for when they sit inside asm).
+
     python tools/check_dpp_hazards.py path/to/file.s [kernel-substring]
 Exit status 1 if any hazard is found.
 """
@@ -93,6 +97,31 @@ def valu_dst(t: str) -> set:
     if o.startswith("v_") and not o.startswith(("v_readfirstlane", "v_readlane", "v_cmp")):
         return regs(t[len(o):].split(",")[0])
     return set()
+
+
+def exec_dpp_hazards(insts, want: str):
+    """3. A DPP instruction fewer than 5 wait states after an EXEC write inside inline asm
+    (the EXEC switch of a broadcast): conservative, the compiler cannot pad for the asm's."""
+    bad = []
+    for i, (k, t, asm, lab) in enumerate(insts):
+        if lab or "_dpp" not in t.split()[0] or (want and want not in (k or "")):
+            continue
+        states, j = 0, i - 1
+        while j >= 0 and states < 5:
+            kk, tt, a, ll = insts[j]
+            if kk != k or ll:
+                break
+            o = tt.split()[0]
+            if o == "s_nop":
+                states += int(tt.split()[1], 0) + 1
+                j -= 1
+                continue
+            if a and re.match(r"s_\S+\s+exec\b", tt):
+                bad.append(f"EXEC→DPP HAZARD in {k}:\n   {tt}\n   {t}  ({states} wait states between)")
+                break
+            states += 1
+            j -= 1
+    return bad
 
 
 def wait_state_hazards(insts, want: str):
@@ -222,6 +251,7 @@ def main(argv=None):
     want = argv[1] if len(argv) > 1 else ""
     insts = parse(path)
     w, wc = wait_state_hazards(insts, want)
+    w += exec_dpp_hazards(insts, want)
     x, xc = narrowed_exec_hazards(insts, want)
     for msg in (w + x)[:50]:
         print(msg)
