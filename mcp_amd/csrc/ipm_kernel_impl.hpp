@@ -80,7 +80,9 @@
 #define MCPX_STAMPS 0
 #endif
 #define MCPX_NSTAMP 6  // residuals | ‖F‖∞ + rr | Schur form | LU / GJ | back-substitution | line search + update
-#if MCPX_STAMPS
+// MCPX_STAMPS=2 (tools/timeline.hip): the wave's start and end on the 100 MHz constant clock
+// and where it ran (HW_ID, XCC_ID) instead — the residency timeline of a launch.
+#if MCPX_STAMPS == 1
 #define MCPX_STAMP(i)                                 \
   do {                                                \
     const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
@@ -1064,6 +1066,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   if constexpr (PASS == 2) {
     if (__builtin_amdgcn_readfirstlane(args.status[blockIdx.x]) != STATUS_DEFERRED) return;
   }
+#if MCPX_STAMPS == 2
+  const uint64_t tl_start = __builtin_amdgcn_s_memrealtime();
+#endif
   if constexpr (MCPX_PRIO > 0) {
     // VALU issue on a SIMD is arbitrated by priority, then age: with equal priorities the
     // oldest resident wave wins, so the waves dispatched last — the ones that set the end of
@@ -1146,7 +1151,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   int outer = 1;                       // :70
   int newton = 0;
   unsigned reason = 0;  // MCPX_FAIL_* events
-#if MCPX_STAMPS
+#if MCPX_STAMPS == 1
   uint64_t st_acc[MCPX_NSTAMP] = {};
   uint64_t st_last = __builtin_amdgcn_s_memtime();
 #endif
@@ -1369,9 +1374,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       if (lane == 0) args.active_mask[inst] = act >> n;
     }
   }
-#if MCPX_STAMPS
+#if MCPX_STAMPS == 1
   if (lane == 0 && args.stamps)
     for (int i = 0; i < MCPX_NSTAMP; ++i) args.stamps[inst * MCPX_NSTAMP + i] = st_acc[i];
+#elif MCPX_STAMPS == 2
+  if (lane == 0 && args.stamps) {
+    uint64_t* t = args.stamps + inst * MCPX_NSTAMP;
+    t[0] = tl_start;
+    t[1] = __builtin_amdgcn_s_memrealtime();
+    t[2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    t[3] = (uint64_t)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+    t[4] = PASS;
+  }
 #endif
   if (lane == 0) {
     args.kkt_error[inst] = kkt;

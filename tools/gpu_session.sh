@@ -9,6 +9,7 @@
 #   driver                the driver's bench command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   bench=<name>:<args>   one bench line, args comma-separated (bench=c4:--lane-change,2)
 #   prof=<name>:<args>    tools/gpu_profile.sh: bench line + rocprofv3 trace + PMC passes
+#   timeline=<args>       tools/timeline.py (residency timeline of a SCHUR launch), args comma-separated
 #   shard                 the per-GPU shards of the strong-scaling configs (C3 2/4/8, C5 512, C4 128)
 #
 # Outputs go to gpurun_out/<out-dir-name>/ (prof steps: gpurun_out/prof_<name>/).  Every GPU
@@ -43,6 +44,10 @@ for step in "$@"; do
       spec=${step#prof=}; name=${spec%%:*}; args=${spec#*:}
       [ "$args" = "$spec" ] && args=""
       bash tools/gpu_profile.sh "$name" ${args//,/ } || exit 7 ;;
+    timeline=*)
+      args=${step#timeline=}
+      timeout -k 10 300 python -u tools/timeline.py ${args//,/ } --out "$O" > "$O/timeline.log" 2>&1 || { tail -20 "$O/timeline.log"; exit 9; }
+      cut -c1-600 "$O/timeline.log" ;;
     shard)
       for G in 32768 16384 8192; do
         timeout -k 10 300 python bench.py --gpus 1 --global-batch $G --steps 20 --warmup 5 --cpu-sample 0 --host-runs 0 > "$O/bench_g$G.json" 2> "$O/bench_g$G.err" || exit 8
