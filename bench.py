@@ -45,7 +45,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (MI355X_MICROAR
 HBM_PEAK_GBS = 8000.0
 XCDS, SIMDS = 8, 256 * 4  # MI355X: 8 XCDs, 256 CUs × 4 SIMDs
 # rocprofv3 evidence of this round's kernels (tools/gpu_profile.sh + tools/prof_summary.py)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
 DEFAULT_GLOBAL = {"c3": 65536, "c5": 4096, "c4": 1024}
 QP_FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters")
 C4_FIELDS = QP_FIELDS
@@ -263,7 +263,7 @@ def launch_ranks(nranks: int, script: str, argv, have_devices: int | None = None
 
 
 def evidence(name: str, cfg: dict) -> dict:
-    """The committed rocprofv3 summaries of this configuration (profiles/r03/
+    """The committed rocprofv3 summaries of this configuration (profiles/r04/
     trace_<name>.json, pmc_<name>.json; tools/prof_summary.py), if they were taken on
     exactly this configuration and this build of libmcpx.so; else {}."""
     from mcp_amd.build import built_hash

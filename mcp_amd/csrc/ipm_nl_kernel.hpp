@@ -86,19 +86,121 @@ constexpr uint64_t remaining_lanes() {
   return m;
 }
 
+#ifndef MCPX_NL_FIX
+#define MCPX_NL_FIX 1  // a violated guess is repaired at its step (0: the whole solve falls back)
+#endif
+
+// Exchange positions K = 16·Jk + Rk and q = 16·JQ + Rq (Rq uniform) of a per-position
+// register array: `addr` = the byte address of the partner lane (lanes Rk ↔ Rq of every DPP
+// row, the others themselves).  JQ is a template argument (the caller dispatches on the
+// uniform half index), so every index is static and the arrays stay in VGPRs.
+__device__ __forceinline__ double bperm_any(double v, int addr) { return bperm_f64_addr(v, addr); }
+__device__ __forceinline__ int bperm_any(int v, int addr) { return __builtin_amdgcn_ds_bpermute(addr, v); }
+template <int NJ, int Jk, int Rk, int JQ, class T>
+__device__ __forceinline__ void swap_positions(T (&v)[NJ], int Rq, int addr, int lc) {
+  const T t1 = bperm_any(v[JQ], addr);  // position q's entry, at K's lanes
+  const T t2 = bperm_any(v[Jk], addr);  // position K's entry, at q's lanes
+  if (lc == Rk) v[Jk] = t1;
+  if (lc == Rq) v[JQ] = t2;
+}
+template <int NM, int K, int JQ>
+__device__ __forceinline__ void lu2d_swap(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
+                                          int (&pv)[Lu2d<NM>::NJ], double (&col)[Lu2d<NM>::NJ], int Rq, int addr,
+                                          int lc) {
+  constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
+  constexpr int Jk = K >> 4, Rk = K & 15, Ck = K >> 2;
+#pragma unroll
+  for (int c = Ck; c < NCB; ++c) {
+    double v[NJ];
+#pragma unroll
+    for (int J = 0; J < NJ; ++J) v[J] = acc[J][c];
+    swap_positions<NJ, Jk, Rk, JQ>(v, Rq, addr, lc);
+#pragma unroll
+    for (int J = 0; J < NJ; ++J) acc[J][c] = v[J];
+  }
+  swap_positions<NJ, Jk, Rk, JQ>(rh, Rq, addr, lc);
+  swap_positions<NJ, Jk, Rk, JQ>(col, Rq, addr, lc);
+  swap_positions<NJ, Jk, Rk, JQ>(pv, Rq, addr, lc);
+}
+
+// Position K's guessed pivot broke the first-max rule: search column K over the remaining
+// positions q ≥ K as the oracle does (largest |a_qk|, ties to the lowest row index p_q) and
+// swap that position's row into position K — its entries in the columns still live (blocks
+// ≥ K / 4), its rhs, its row index and its column-K entry — then take the new pivot and its
+// reciprocal.  The elimination then goes on exactly as if the guess had been right, so a
+// wrong guess costs ~one swap instead of a second, searched factorisation.  A NaN among the
+// candidates or an all-zero column sets `bad` (the searched Gauss-Jordan decides those).
+template <int NM, int K>
+__device__ __forceinline__ void lu2d_fix(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
+                                         int (&pv)[Lu2d<NM>::NJ], double (&col)[Lu2d<NM>::NJ], double& piv,
+                                         double& rp, bool& bad, int ln) {
+  constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
+  constexpr int Jk = K >> 4, Rk = K & 15, Ck = K >> 2, Qk = K & 3;
+  constexpr uint64_t RK[4] = {remaining_lanes<NM, K - 1, 0>(), remaining_lanes<NM, K - 1, 1>(),
+                              remaining_lanes<NM, K - 1, 2>(), remaining_lanes<NM, K - 1, 3>()};
+  const int lc = ln & 15;
+  double mloc = 0.0;
+  bool nan = false;
+#pragma unroll
+  for (int J = Jk; J < NJ; ++J) {
+    if (RK[J & 3] == 0) continue;
+    const bool live = (RK[J & 3] >> lc) & 1;
+    const double av = fabs(col[J]);
+    nan |= live && (av != av);
+    if (live && av > mloc) mloc = av;
+  }
+  const double mx = wave_max_nonneg(nan ? 0.0 : mloc);
+  if (ballot(nan) != 0ull || !(mx > 0.0)) {
+    bad = true;
+    return;
+  }
+  uint32_t key = 0u;  // ~p_q of the candidates: the wave max is the lowest row index
+#pragma unroll
+  for (int J = Jk; J < NJ; ++J) {
+    if (RK[J & 3] == 0) continue;
+    const bool live = (RK[J & 3] >> lc) & 1;
+    if (live && fabs(col[J]) == mx) key = max(key, ~(uint32_t)pv[J]);
+  }
+  const uint32_t pbest = ~wave_max_u32(key);
+  int qs = K;
+#pragma unroll
+  for (int J = NJ - 1; J >= Jk; --J) {
+    if (RK[J & 3] == 0) continue;
+    const uint64_t b = ballot((uint32_t)pv[J] == pbest) & RK[J & 3];
+    if (b) qs = 16 * J + lowest_lane(b);
+  }
+  qs = __builtin_amdgcn_readfirstlane(qs);
+  if (qs != K) {
+    const int Jq = qs >> 4, Rq = qs & 15;
+    const int addr = ((ln & 48) | (lc == Rk ? Rq : (lc == Rq ? Rk : lc))) << 2;
+    // q > K, so its half is Jk or later (static dispatch on the uniform half index)
+    if (Jq == Jk) lu2d_swap<NM, K, Jk>(acc, rh, pv, col, Rq, addr, lc);
+    else if constexpr (Jk + 1 < NJ) {
+      if (Jq == Jk + 1) lu2d_swap<NM, K, (Jk + 1 < NJ ? Jk + 1 : Jk)>(acc, rh, pv, col, Rq, addr, lc);
+      else if constexpr (Jk + 2 < NJ) {
+        if (Jq == Jk + 2) lu2d_swap<NM, K, (Jk + 2 < NJ ? Jk + 2 : Jk)>(acc, rh, pv, col, Rq, addr, lc);
+        else if constexpr (Jk + 3 < NJ) lu2d_swap<NM, K, (Jk + 3 < NJ ? Jk + 3 : Jk)>(acc, rh, pv, col, Rq, addr, lc);
+      }
+    }
+  }
+  piv = bcast(acc[Jk][Ck], 16 * Qk + Rk);
+  rp = rcp_fast(piv);
+}
+
 // Step K with one step of lookahead: `piv` (uniform), its reciprocal `rp` and `col` (column
 // K by position, from ds_bpermute) were produced by step K − 1 right after it updated column
 // K, so the LDS latency and the reciprocal's 7-deep dependent chain hide behind the rest of
-// that step's update.  Step K updates the column block of column K + 1 first, fetches pivot
-// K + 1, starts its reciprocal and fetches its column, then updates the other blocks.  Each
-// entry still takes the same fma in the same order.  1 / piv is the uniform fast reciprocal
-// with no branch: a pivot that is zero, NaN or outside its exact range only sets `bad`, the
-// remaining steps run on (discarded) values, and the caller falls back to the searched
-// Gauss-Jordan.  The first-max check of the guess is three compares per half into lane
-// masks (|a_qk| > |piv| or NaN; equal with a lower row index), on the remaining positions.
+// that step's update.  Step K first checks the guessed pivot against the first-max rule over
+// the remaining positions (three compares per half into lane masks: |a_qk| > |piv| or NaN;
+// equal with a lower row index) and repairs a violation in place (lu2d_fix).  It then
+// updates the column block of column K + 1, fetches pivot K + 1, starts its reciprocal and
+// fetches its column, then updates the other blocks.  Each entry still takes the same fma
+// in the same order.  1 / piv is the uniform fast reciprocal with no branch: a pivot that is
+// zero, NaN or outside its exact range only sets `bad`, the remaining steps run on
+// (discarded) values, and the caller falls back to the searched Gauss-Jordan.
 template <int NM, int K>
 __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
-                                          const int (&pv)[Lu2d<NM>::NJ], int pkk, int ln, uint64_t& viol,
+                                          int (&pv)[Lu2d<NM>::NJ], int ln, uint64_t& viol,
                                           double& rpv, bool& bad, double& piv, double& rp,
                                           double (&col)[Lu2d<NM>::NJ]) {
   constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
@@ -107,29 +209,37 @@ __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::
   constexpr int Jn = (K + 1) >> 4, Rn = (K + 1) & 15, Qn = (K + 1) & 3, Cn = (K + 1) >> 2;
   __builtin_amdgcn_sched_barrier(0);  // one step at a time: no step's uniform values hoisted ahead
   const int lc = ln & 15;
+  {  // the first-max rule over the remaining positions
+    const int pkk = __builtin_amdgcn_readlane(pv[Jk], Rk);
+    const double ap = fabs(piv);
+    uint64_t vk = 0;
+#pragma unroll
+    for (int J = 0; J < NJ; ++J) {
+      constexpr uint64_t REM[4] = {remaining_lanes<NM, K, 0>(), remaining_lanes<NM, K, 1>(),
+                                   remaining_lanes<NM, K, 2>(), remaining_lanes<NM, K, 3>()};
+      if (J >= Jk && REM[J & 3] != 0) {
+        const double av = fabs(col[J]);
+        vk |= (ballot(!(av <= ap)) | (ballot(av == ap) & ballot(pv[J] < pkk))) & REM[J & 3];
+      }
+    }
+    if constexpr (MCPX_NL_FIX) {
+      if (vk != 0ull) lu2d_fix<NM, K>(acc, rh, pv, col, piv, rp, bad, ln);
+    } else {
+      viol |= vk;
+    }
+    bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
+  }
   if (ln == K) rpv = rp;
-  const double ap = fabs(piv);
   double nlm[NJ];
 #pragma unroll
-  for (int J = 0; J < NJ; ++J) {
-    const double v = col[J];  // a_qk of position q = lc + 16J
-    const int q = lc + 16 * J;
-    constexpr uint64_t REM[4] = {remaining_lanes<NM, K, 0>(), remaining_lanes<NM, K, 1>(),
-                                 remaining_lanes<NM, K, 2>(), remaining_lanes<NM, K, 3>()};
-    if (J >= Jk && REM[J & 3] != 0) {  // the first-max rule over the remaining positions
-      const double av = fabs(v);
-      viol |= (ballot(!(av <= ap)) | (ballot(av == ap) & ballot(pv[J] < pkk))) & REM[J & 3];
-    }
-    // Gauss-Jordan: every position but the pivot's, remaining or not; the pivot row +0
-    nlm[J] = ((q != K) & (q < NM)) ? -(v * rp) : 0.0;
-  }
+  for (int J = 0; J < NJ; ++J) nlm[J] = -(col[J] * rp);  // padding positions: col = 0, rows stay 0
+  nlm[Jk] = zero_lanes<Rk>(nlm[Jk]);  // the pivot row: multiplier +0
   if constexpr (NX) {  // column block of column K + 1, then pivot K + 1, its reciprocal and column
 #pragma unroll
     for (int J = 0; J < NJ; ++J)
       if (J != Jk) fmac_row_bcast<Rk, false>(acc[J][Cn], acc[Jk][Cn], nlm[J]);
     fmac_row_bcast_self<Rk, false>(acc[Jk][Cn], nlm[Jk]);
     piv = bcast(acc[Jn][Cn], 16 * Qn + Rn);
-    bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
     rp = rcp_fast(piv);
 #pragma unroll
     for (int J = 0; J < NJ; ++J) col[J] = bperm_f64_addr(acc[J][Cn], (16 * Qn + lc) << 2);
@@ -155,20 +265,19 @@ __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::
 template <int NM, int... K>
 __device__ __forceinline__ void lu2d_steps(std::integer_sequence<int, K...>,
                                            double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
-                                           const int (&pv)[Lu2d<NM>::NJ], int pk, int ln, uint64_t& viol, double& rpv,
+                                           int (&pv)[Lu2d<NM>::NJ], int ln, uint64_t& viol, double& rpv,
                                            bool& bad) {
   constexpr int NJ = Lu2d<NM>::NJ;
   const int lc = ln & 15;
   double piv = bcast(acc[0][0], 0), col[NJ];  // pivot 0, its reciprocal and column 0
-  bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
   double rp = rcp_fast(piv);
 #pragma unroll
   for (int J = 0; J < NJ; ++J) col[J] = bperm_f64_addr(acc[J][0], lc << 2);
-  (lu2d_step<NM, K>(acc, rh, pv, __builtin_amdgcn_readlane(pk, K), ln, viol, rpv, bad, piv, rp, col), ...);
+  (lu2d_step<NM, K>(acc, rh, pv, ln, viol, rpv, bad, piv, rp, col), ...);
 }
 
 template <int NM>
-__device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk, double& dz) {
+__device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int& pk, double& dz) {
   constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
   const int lr = ln >> 4, lc = ln & 15;
   double acc[NJ][NCB], rh[NJ];
@@ -186,8 +295,18 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int pk
   uint64_t viol = 0;
   double rpv = 0.0;
   bool bad = false;
-  lu2d_steps<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, pv, pk, ln, viol, rpv, bad);
+  lu2d_steps<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, pv, ln, viol, rpv, bad);
   if (bad || viol != 0) return false;
+  if constexpr (MCPX_NL_FIX) {  // the pivot sequence taken (repairs included): next step's guess
+    int t[NJ];
+#pragma unroll
+    for (int J = 0; J < NJ; ++J) t[J] = __builtin_amdgcn_ds_bpermute(lc << 2, pv[J]);
+    int p = t[0];
+#pragma unroll
+    for (int J = 1; J < NJ; ++J)
+      if (lr == J) p = t[J];
+    pk = p;
+  }
   // x_k = b_k · (1 / u_kk): lane k = (lr, lc) holds position lc + 16·lr = k in rh[lr]
   double r = rh[0];
 #pragma unroll
