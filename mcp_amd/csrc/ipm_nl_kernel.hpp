@@ -89,6 +89,9 @@ constexpr uint64_t remaining_lanes() {
 #ifndef MCPX_NL_FIX
 #define MCPX_NL_FIX 1  // a violated guess is repaired at its step (0: the whole solve falls back)
 #endif
+#ifndef MCPX_NL_PREC
+#define MCPX_NL_PREC 1  // pivots recorded by v_writelane; range check and 1/u_kk once at the end
+#endif
 
 // Exchange positions K = 16·Jk + Rk and q = 16·JQ + Rq (Rq uniform) of a per-position
 // register array: `addr` = the byte address of the partner lane (lanes Rk ↔ Rq of every DPP
@@ -195,9 +198,11 @@ __device__ __forceinline__ void lu2d_fix(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::N
 // equal with a lower row index) and repairs a violation in place (lu2d_fix).  It then
 // updates the column block of column K + 1, fetches pivot K + 1, starts its reciprocal and
 // fetches its column, then updates the other blocks.  Each entry still takes the same fma
-// in the same order.  1 / piv is the uniform fast reciprocal with no branch: a pivot that is
-// zero, NaN or outside its exact range only sets `bad`, the remaining steps run on
-// (discarded) values, and the caller falls back to the searched Gauss-Jordan.
+// in the same order.  1 / piv is the uniform fast reciprocal with no branch; the pivot itself
+// goes to lane K (v_writelane, MCPX_NL_PREC), and after the last step every lane checks its
+// pivot at once: one that is zero, NaN or outside the reciprocal's exact range means the
+// remaining steps ran on (discarded) values, and the caller falls back to the searched
+// Gauss-Jordan.  Lane k's 1 / u_kk for x_k is taken there too, all lanes at once.
 template <int NM, int K>
 __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::NCB], double (&rh)[Lu2d<NM>::NJ],
                                           int (&pv)[Lu2d<NM>::NJ], int ln, uint64_t& viol,
@@ -223,13 +228,16 @@ __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::
       }
     }
     if constexpr (MCPX_NL_FIX) {
-      if (vk != 0ull) lu2d_fix<NM, K>(acc, rh, pv, col, piv, rp, bad, ln);
+      // unlikely: the repair's code goes out of the steps' straight line (taken on every step, the
+      // branch around it cost 6 %: profiles/r04/ab_c4_repair_layout.jsonl)
+      if (__builtin_expect(vk != 0ull, 0)) lu2d_fix<NM, K>(acc, rh, pv, col, piv, rp, bad, ln);
     } else {
       viol |= vk;
     }
-    bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
+    if constexpr (!MCPX_NL_PREC) bad |= !(fabs(piv) > 0.0) || !rcp_fast_ok(piv);
   }
-  if (ln == K) rpv = rp;
+  if constexpr (MCPX_NL_PREC) rpv = writelane_f64(rpv, piv, K);  // lane K: pivot K (1 / u_kk at the end)
+  else if (ln == K) rpv = rp;
   double nlm[NJ];
 #pragma unroll
   for (int J = 0; J < NJ; ++J) nlm[J] = -(col[J] * rp);  // padding positions: col = 0, rows stay 0
@@ -296,6 +304,10 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int& p
   double rpv = 0.0;
   bool bad = false;
   lu2d_steps<NM>(std::make_integer_sequence<int, NM>{}, acc, rh, pv, ln, viol, rpv, bad);
+  if constexpr (MCPX_NL_PREC) {  // lane k holds pivot k: the range check and 1 / u_kk, all lanes at once
+    bad |= ballot(ln < NM && !((fabs(rpv) > 0.0) & rcp_fast_ok(rpv))) != 0ull;
+    rpv = rcp_fast(rpv);
+  }
   if (bad || viol != 0) return false;
   if constexpr (MCPX_NL_FIX) {  // the pivot sequence taken (repairs included): next step's guess
     int t[NJ];
