@@ -1,7 +1,7 @@
 """A/B of compile-time variants of the C4 lane-change module (T = 2, SCHUR, one wave).
 
-Build (CPU, here):   python tools/ab_c4/variants.py build NAME=-DFLAG=1[,-DFLAG2=0] ...
-Run (GPU box):       python tools/ab_c4/variants.py run NAME ... [--out file.jsonl]
+Build (CPU, here):   python tools/ab_c4/variants.py build NAME=-DFLAG=1[,-DFLAG2=0] ... [--T 2]
+Run (GPU box):       python tools/ab_c4/variants.py run NAME ... [--out file.jsonl] [--T 2]
 
 `build` compiles the product module's generated .hip with the module flags of
 mcp_amd/codegen.py plus the variant's -D flags into tools/ab_c4/<NAME>.hsaco (not kept in
@@ -23,10 +23,13 @@ sys.path.insert(0, ROOT)
 FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters")
 
 
+T = 2  # horizon (--T)
+
+
 def game():
     from mcp_amd.lane_change import LaneChangeGame
 
-    return LaneChangeGame(2)
+    return LaneChangeGame(T)
 
 
 def build(specs):
@@ -63,7 +66,8 @@ def run(names, out_path=None):
     recs = []
     for name, mod in mods.items():
         out = alloc_device_outputs(1024, n, m, th.device)
-        go = lambda: solve_batch_device(_abi.FAMILY_NONLINEAR, n, m, th, out, tol=1e-6, linear_solver="schur", module=mod)
+        go = lambda: solve_batch_device(_abi.FAMILY_NONLINEAR, n, m, th, out, tol=1e-6,
+                                        linear_solver=mcp.nl.default_solver(), module=mod)
         go()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -91,6 +95,10 @@ def run(names, out_path=None):
 if __name__ == "__main__":
     mode, rest = sys.argv[1], sys.argv[2:]
     outp = None
+    if "--T" in rest:
+        i = rest.index("--T")
+        T = int(rest[i + 1])
+        rest = rest[:i] + rest[i + 2:]
     if "--out" in rest:
         i = rest.index("--out")
         outp = rest[i + 1]
