@@ -1,12 +1,17 @@
 // Diagnostic: per-phase s_memtime cycles of a generated nonlinear module's one-wave kernel
 // (module built with -DMCPX_STAMPS=1; see tools/nl_phase.py, which writes θ and runs this).
 //   nl_phase <module.hsaco> <kernel> <theta.bin> n m p B [threads per instance: 64, or 256 for _mw]
+// A kernel name ending in "_wg" runs the workgroup-per-instance kernel the way the C ABI does
+// (csrc/mcpx_api.cpp launch_wg: resident grid, atomic work queue, per-slot workspace).
 #include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
 #include "../mcp_amd/csrc/ipm_kernel.h"
+#include "../mcp_amd/csrc/ipm_wg.h"
 
 int main(int argc, char** argv) {
   if (argc < 8) { fprintf(stderr, "usage\n"); return 2; }
@@ -41,12 +46,44 @@ int main(int argc, char** argv) {
   for (int k = 0; k <= a.max_inner; ++k) { a.tight[k] = 1 - exp(-0.1 * k); a.loose[k] = 1 + exp(-0.5 * k); }
   size_t sz = sizeof a;
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  const size_t kl = strlen(kname);
+  const bool wg = kl > 3 && !strcmp(kname + kl - 3, "_wg");
+  mcpx::wg::WgArgs w{};
+  size_t wsz = sizeof w;
+  void* wcfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &w, HIP_LAUNCH_PARAM_BUFFER_SIZE, &wsz, HIP_LAUNCH_PARAM_END};
+  unsigned grid = (unsigned)B;
+  if (wg) {  // as launch_wg: SCHUR, ns = n
+    int32_t meta[12] = {};
+    hipDeviceptr_t mp;
+    size_t mb = 0;
+    if (hipModuleGetGlobal(&mp, &mb, M, "mcpx_nl_meta") != hipSuccess) { fprintf(stderr, "no mcpx_nl_meta\n"); return 2; }
+    (void)hipMemcpy(meta, (void*)mp, std::min(mb, sizeof meta), hipMemcpyDeviceToHost);
+    int per_cu = 0, cus = 0;
+    (void)hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, K, threads, 0);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    auto align = [](int64_t v) { return (v + 31) / 32 * 32; };
+    const int ns = n;
+    w.ld = ns + 1;
+    w.off_blk = align((int64_t)ns * w.ld);
+    w.off_rd = align(w.off_blk + meta[6]);
+    w.off_aux = align(w.off_rd + (int64_t)m * n);
+    w.slot_stride = align(w.off_aux + 4 * (int64_t)m);
+    grid = (unsigned)std::min<int64_t>((int64_t)std::max(per_cu, 1) * std::max(cus, 1), B);
+    double* ws = nullptr;
+    (void)hipMalloc(&ws, sizeof(double) * (size_t)(grid * w.slot_stride) + 256);
+    w.work = ws;
+    w.counter = (int32_t*)(ws + grid * w.slot_stride);
+    w.batch = B;
+    w.k = a;
+    printf("workgroup kernel: %d per CU, grid %u, slot %lld doubles\n", per_cu, grid, (long long)w.slot_stride);
+  }
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   float ms = 0;
   for (int rep = 0; rep < 2; ++rep) {
     (void)hipEventRecord(e0, 0);
-    if (hipModuleLaunchKernel(K, B, 1, 1, threads, 1, 1, 0, 0, nullptr, cfg) != hipSuccess) { fprintf(stderr, "launch failed\n"); return 2; }
+    if (wg) (void)hipMemset(w.counter, 0, 4);
+    if (hipModuleLaunchKernel(K, grid, 1, 1, threads, 1, 1, 0, 0, nullptr, wg ? wcfg : cfg) != hipSuccess) { fprintf(stderr, "launch failed\n"); return 2; }
     (void)hipEventRecord(e1, 0);
     (void)hipDeviceSynchronize();
     (void)hipEventElapsedTime(&ms, e0, e1);
