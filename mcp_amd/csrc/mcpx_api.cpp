@@ -299,8 +299,8 @@ int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const d
   mcpx::wg::WgArgs w{};
   w.ld = ns + 1;
   w.off_blk = align((int64_t)ns * w.ld);
-  w.off_rd = align(w.off_blk + (mod ? mod->meta[6] : 0));
-  w.off_aux = align(w.off_rd + (ls == MCPX_LINSOLVE_SCHUR ? (int64_t)m * n : 0));
+  w.off_aux = align(w.off_blk + (mod ? mod->meta[6] : 0));
+  w.off_rd = w.off_aux;  // (R·D⁻¹ no longer kept: the SCHUR entries read R and D⁻¹ directly)
   w.slot_stride = align(w.off_aux + (ls == MCPX_LINSOLVE_SCHUR ? 4 * (int64_t)m : 0));
   const int64_t CH = (int64_t)1 << 30;
   const int64_t grid_max = std::min(slots_max, std::min(CH, d->batch));

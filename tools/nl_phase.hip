@@ -65,8 +65,8 @@ int main(int argc, char** argv) {
     const int ns = n;
     w.ld = ns + 1;
     w.off_blk = align((int64_t)ns * w.ld);
-    w.off_rd = align(w.off_blk + meta[6]);
-    w.off_aux = align(w.off_rd + (int64_t)m * n);
+    w.off_aux = align(w.off_blk + meta[6]);
+    w.off_rd = w.off_aux;
     w.slot_stride = align(w.off_aux + 4 * (int64_t)m);
     grid = (unsigned)std::min<int64_t>((int64_t)std::max(per_cu, 1) * std::max(cus, 1), B);
     double* ws = nullptr;
