@@ -65,6 +65,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(mode, "gen64")) e = mcpx::launch_one<64, 0, 0, 0, MCPX_LINSOLVE_REDUCED>(a, B, 0);
     else if (!strcmp(mode, "dense")) e = mcpx::launch_one<64, 0, 0, 0, MCPX_LINSOLVE_DENSE>(a, B, 0);
     else if (!strcmp(mode, "schur") && n == 32 && m == 16) e = mcpx::launch_one<32, 0, 32, 16, MCPX_LINSOLVE_SCHUR>(a, B, 0);
+    else if (!strcmp(mode, "schur") && n == 16 && m == 8) e = mcpx::launch_one<16, 0, 16, 8, MCPX_LINSOLVE_SCHUR>(a, B, 0);
     else if (!strcmp(mode, "schurgen") && n <= 32) e = mcpx::launch_one<32, 0, 0, 0, MCPX_LINSOLVE_SCHUR>(a, B, 0);
     if (e != hipSuccess) { printf("launch failed / unsupported mode: %s\n", hipGetErrorString(e)); return 1; }
     (void)hipDeviceSynchronize();
