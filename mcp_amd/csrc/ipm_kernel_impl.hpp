@@ -54,6 +54,12 @@
 #define MCPX_LDS_A 1
 #endif
 
+// SCHUR kernels with compile-time n ≤ 16 (C2) keep M in LDS as well (A/B knob): its 2 KB per
+// wave fit beside A at the occupancy those kernels run at.
+#ifndef MCPX_LDS_M
+#define MCPX_LDS_M 0
+#endif
+
 // kkt and ϵ re-read into SGPRs after each update (A/B knob).
 #ifndef MCPX_SREG_KKT
 #define MCPX_SREG_KKT 0
@@ -1091,6 +1097,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   constexpr bool LDSA = SCH && NC > 0 && MC > 0 && MCPX_LDS_A;
   constexpr int LDA = LDSA ? MC + 1 : 1;
   __shared__ double sA[LDSA ? NC * LDA + MC + NC : 1];
+  constexpr bool LDSM = LDSA && NC <= 16 && MCPX_LDS_M;  // M (column-major, as in θ) in LDS too
+  __shared__ double sM[LDSM ? NC * NC : 1];
   const int lane = threadIdx.x;
   const int64_t inst = blockIdx.x;
   const int n0 = NC ? NC : args.n, m0 = MC ? MC : args.m;
@@ -1115,6 +1123,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
 #pragma unroll
     for (int i = lane; i < NC * MC; i += 64) sA[(i / MC) * LDA + i % MC] = tg[i];
     for (int i = lane; i < MC + NC; i += 64) sA[NC * LDA + i] = tg[NC * MC + i];
+  }
+  if constexpr (LDSM) {
+#pragma unroll
+    for (int i = lane; i < NC * NC; i += 64) sM[i] = th0[i];
   }
 
   // SCHUR: M exactly symmetric ⇒ S symmetric ⇒ try the pivot-free SPD
@@ -1166,6 +1178,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       // SCHUR: the A block (then b, ϕ), from the wave's LDS copy when it has one
       const double* const ta = LDSA ? (const double*)sA : th + n * n;
       const int lda = LDSA ? LDA : m;
+      const double* const tm = LDSM ? (const double*)sM : th;  // the M block
       const int ln = opaque_lane(lane);
       // ---- F!, ∇F_z! (:79-81) --------------------------------------------
       __syncthreads();
@@ -1179,7 +1192,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       // quotient-per-use form costs (8 of them in the Schur K-loop).
       double rw = 1.0, Di = 1.0, ryr = 0.0;
       if constexpr (SCH) {
-        qp_residuals<MCPX_RES_BATCH>(th, ta, lda, zs, ln, n, m, eps, s, F, Fc);
+        qp_residuals<MCPX_RES_BATCH>(tm, ta, lda, zs, ln, n, m, eps, s, F, Fc);
         rhs = -F;
         if (rh) {  // eliminate δs_k (pivot w_k) and then δy_k (pivot D_k)
           w = zs[ln] + tol;
@@ -1216,7 +1229,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         constexpr int NT = (NMAX + 15) / 16;
         if (spd_try) {  // S formed transposed on the matrix cores, Gauss-Jordan in that layout
           d4 acc4[NT][NT];
-          qp_schur_form_2d<NT>(th, ta, lda, sD, ln, n, m, tol, acc4);
+          qp_schur_form_2d<NT>(tm, ta, lda, sD, ln, n, m, tol, acc4);
           MCPX_STAMP(2);
           double acc[NT][NT][4];
 #pragma unroll
@@ -1246,7 +1259,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
           // ds_bpermute: no n×n LDS tile, so LDS (2 KB per wave) does not cap occupancy
           constexpr int NT = (NMAX + 15) / 16;
           d4 acc4[NT][NT];
-          qp_schur_form_2d<NT>(th, ta, lda, sD, ln, n, m, tol, acc4);
+          qp_schur_form_2d<NT>(tm, ta, lda, sD, ln, n, m, tol, acc4);
           schur_rows_from_2d<NT, NMAX>(acc4, ln, n, a);
           rhs = sB[ln];
           ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);

@@ -89,6 +89,12 @@ constexpr uint64_t remaining_lanes() {
 #ifndef MCPX_NL_FIX
 #define MCPX_NL_FIX 1  // a violated guess is repaired at its step (0: the whole solve falls back)
 #endif
+#ifndef MCPX_NL_SCOL
+#define MCPX_NL_SCOL 1  // one-wave SCHUR: S column-major in LDS (the P copy is a straight b128 copy)
+#endif
+#ifndef MCPX_NL_SEHOIST
+#define MCPX_NL_SEHOIST 1  // the Schur-entry tables in VGPRs for the whole solve
+#endif
 #ifndef MCPX_NL_PREC
 #define MCPX_NL_PREC 1  // pivots recorded by v_writelane; range check and 1/u_kk once at the end
 #endif
@@ -284,7 +290,7 @@ __device__ __forceinline__ void lu2d_steps(std::integer_sequence<int, K...>,
   (lu2d_step<NM, K>(acc, rh, pv, ln, viol, rpv, bad, piv, rp, col), ...);
 }
 
-template <int NM>
+template <int NM, bool COL = false>
 __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int& pk, double& dz) {
   constexpr int NJ = Lu2d<NM>::NJ, NCB = Lu2d<NM>::NCB;
   const int lr = ln >> 4, lc = ln & 15;
@@ -295,10 +301,17 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int& p
     const int q = lc + 16 * J;
     const int p = __builtin_amdgcn_ds_bpermute(min(q, 63) << 2, pk);  // row p_q of position q
     pv[J] = q < NM ? p : 1 << 20;
-    const double* row = Srow + (q < NM ? p : 0) * LDR;
+    const int pr = q < NM ? p : 0;
+    if constexpr (COL) {
 #pragma unroll
-    for (int c = 0; c < NCB; ++c) acc[J][c] = (q < NM && lr + 4 * c < NM) ? row[lr + 4 * c] : 0.0;
-    rh[J] = q < NM ? row[NM] : 0.0;
+      for (int c = 0; c < NCB; ++c) acc[J][c] = (q < NM && lr + 4 * c < NM) ? Srow[(lr + 4 * c) * NM + pr] : 0.0;
+      rh[J] = q < NM ? Srow[NM * NM + pr] : 0.0;
+    } else {
+      const double* row = Srow + pr * LDR;
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) acc[J][c] = (q < NM && lr + 4 * c < NM) ? row[lr + 4 * c] : 0.0;
+      rh[J] = q < NM ? row[NM] : 0.0;
+    }
   }
   uint64_t viol = 0;
   double rpv = 0.0;
@@ -329,49 +342,77 @@ __device__ __forceinline__ bool lu2d_solve(double* Srow, int LDR, int ln, int& p
 }
 
 // ---- Schur complement into LDS, entry-parallel ---------------------------------------
-// Row i of [S | rr] at Srow[i·LDR], S = (P + tol·I) − Q D⁻¹ R, rr_i = −F_Gi − Σ_k Q_ik ty_k.
+// [S | rr], S = (P + tol·I) − Q D⁻¹ R, rr_i = −F_Gi − Σ_k Q_ik ty_k: row i at Srow[i·LDR], or
+// with COL (the one-wave kernel, MCPX_NL_SCOL) column-major, entry (i, j) at Srow[j·n + i] and
+// rr at Srow[n·n + i] — the layout P has in blk, so P is a straight two-doubles-per-lane copy
+// and the diagonal's + tol a second pass (+6.6 % on the C4 batch with the entry tables held
+// in VGPRs, MCPX_NL_SEHOIST: profiles/r04/ab_c4_formation.jsonl).
 // First P + tol·I and −F_G, one P entry per lane and slot (column-major P: coalesced);
 // then each structural nonzero of Q D⁻¹ R and each rr_i with K(i) ≠ ∅ — an "entry" of the
 // generated tables mcpx_nl_se_pos / mcpx_nl_se_k (codegen.py: slot e = lane + 64r, its
 // position i·LDR + j and its k ascending) — takes its fma chain in one lane:
 // fma(−Q_ik, R_kj·D_k⁻¹, ·) (rr: fma(−Q_ik, ty_k, ·)), k ascending: the oracle's chain
 // for that entry (oracle/ipm_oracle.c, the row-wise loop over K(i) and J(k)).
-template <int LDR>
-__device__ __forceinline__ void schur_form_entries(double* Srow, const double* blk, const double* Fs,
-                                                   const double* sDi, const double* sTy, double tol, int ln) {
-  constexpr int NP = n * n, RP = (NP + 63) / 64;
+struct SeTables {
+  int pos[MCPX_NL_SE_ER], ks[MCPX_NL_SE_ER][MCPX_NL_SE_KT];
+  __device__ __forceinline__ void load(int ln) {
 #pragma unroll
-  for (int r = 0; r < RP; ++r) {
-    const int t = ln + 64 * r;
-    if (t < NP) {
-      const int j = t / n, i = t - j * n;  // P_ij = blk[OFF_P + j·n + i]
-      const double v = blk[OFF_P + t];
-      Srow[i * LDR + j] = (i == j) ? v + tol : v;
+    for (int r = 0; r < MCPX_NL_SE_ER; ++r) {
+      pos[r] = mcpx_nl_se_pos[64 * r + ln];
+#pragma unroll
+      for (int t = 0; t < MCPX_NL_SE_KT; ++t) ks[r][t] = mcpx_nl_se_k[(r * MCPX_NL_SE_KT + t) * 64 + ln];
     }
   }
-  if (ln < n) Srow[ln * LDR + n] = -Fs[ln];
-  __syncthreads();
-  int pos[MCPX_NL_SE_ER], ks[MCPX_NL_SE_ER][MCPX_NL_SE_KT];
+};
+
+// COL: S column-major, entry (i, j) at Srow[j·n + i], the rr column at Srow[n·n + i].
+template <int LDR, bool COL = false>
+__device__ __forceinline__ void schur_form_entries(double* Srow, const double* blk, const double* Fs,
+                                                   const double* sDi, const double* sTy, double tol, int ln,
+                                                   const SeTables* se_in = nullptr) {
+  constexpr int NP = n * n, RP = (NP + 63) / 64;
+  if constexpr (COL) {  // P as it lies in blk (column-major), two doubles per lane and access
+    typedef double d2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-  for (int r = 0; r < MCPX_NL_SE_ER; ++r) {
-    pos[r] = mcpx_nl_se_pos[64 * r + ln];
+    for (int r = 0; r < (NP + 127) / 128; ++r) {
+      const int t = 2 * ln + 128 * r;
+      if (t + 1 < NP) *(d2*)(Srow + t) = *(const d2*)(blk + OFF_P + t);
+      else if (t < NP) Srow[t] = blk[OFF_P + t];
+    }
+    if (ln < n) Srow[NP + ln] = -Fs[ln];
+    __syncthreads();
+    if (ln < n) Srow[ln * n + ln] = Srow[ln * n + ln] + tol;  // the diagonal's + tol (the row-major copy's v + tol)
+  } else {
 #pragma unroll
-    for (int t = 0; t < MCPX_NL_SE_KT; ++t) ks[r][t] = mcpx_nl_se_k[(r * MCPX_NL_SE_KT + t) * 64 + ln];
+    for (int r = 0; r < RP; ++r) {
+      const int t = ln + 64 * r;
+      if (t < NP) {
+        const int j = t / n, i = t - j * n;  // P_ij = blk[OFF_P + j·n + i]
+        const double v = blk[OFF_P + t];
+        Srow[i * LDR + j] = (i == j) ? v + tol : v;
+      }
+    }
+    if (ln < n) Srow[ln * LDR + n] = -Fs[ln];
   }
+  __syncthreads();
+  SeTables own;
+  if (!se_in) own.load(ln);
+  const SeTables& se = se_in ? *se_in : own;
 #pragma unroll
   for (int r = 0; r < MCPX_NL_SE_ER; ++r) {
-    if (pos[r] < 0) continue;
-    const int i = pos[r] / LDR, j = pos[r] - i * LDR;
-    double v = Srow[pos[r]];
+    if (se.pos[r] < 0) continue;
+    const int i = se.pos[r] / LDR, j = se.pos[r] - i * LDR;
+    const int at = COL ? j * n + i : se.pos[r];
+    double v = Srow[at];
 #pragma unroll
     for (int t = 0; t < MCPX_NL_SE_KT; ++t) {
-      const int k = ks[r][t];
+      const int k = se.ks[r][t];
       if (k < 0) continue;
       const double q = -blk[OFF_Q + k * n + i];
       const double f = (j == n) ? sTy[k] : blk[OFF_R + j * m + k] * sDi[k];
       v = fma(q, f, v);
     }
-    Srow[pos[r]] = v;
+    Srow[at] = v;
   }
 }
 
@@ -526,12 +567,13 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   constexpr bool EV = VEC && SCH && !MW;
 #if defined(MCPX_NL_VEC)
   static_assert(!EV || (MCPX_NL_VEC_OFF_Z >= BLK && MCPX_NL_VEC_OFF_T >= MCPX_NL_VEC_OFF_Z + NZ), "ev layout");
-  __shared__ double ev[EV ? MCPX_NL_VEC_EV : 1];
+  __shared__ __attribute__((aligned(16))) double ev[EV ? MCPX_NL_VEC_EV : 1];
   uint32_t vw[MCPX_NL_VEC_NWORD], vd[MCPX_NL_VEC_NSLOT];
 #else
   __shared__ double ev[1];
 #endif
-  __shared__ double blk_own[EV ? 1 : BLK], zs_own[EV ? 1 : NZ];
+  __shared__ __attribute__((aligned(16))) double blk_own[EV ? 1 : BLK];
+  __shared__ double zs_own[EV ? 1 : NZ];
   double* const blk = EV ? ev : blk_own;
 #if defined(MCPX_NL_VEC)
   double* const zs = EV ? ev + MCPX_NL_VEC_OFF_Z : zs_own;
@@ -540,7 +582,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
 #endif
   __shared__ double dzs[NZ], Fs[NZ];
   constexpr int LDR = n + 1;  // SCHUR: lane-private LDS rows of S (odd stride: 2-way bank conflicts at most)
-  __shared__ double Srow[SCH ? imax(1, n * LDR) : 1];
+  __shared__ __attribute__((aligned(16))) double Srow[SCH ? imax(1, n * LDR) : 1];
   __shared__ double sRw[SCH ? MZ : 1], sDi[SCH ? MZ : 1], sRy[SCH ? MZ : 1], sTy[SCH ? MZ : 1];
   constexpr int WV = MW ? 4 : 1;  // waves per instance
   static_assert(!MW || SCH, "the multi-wave kernel is the SCHUR one");
@@ -586,6 +628,8 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
   int outer = 1;                      // :70
   int newton = 0;
   unsigned reason = 0;  // MCPX_FAIL_* events
+  SeTables se_tab;
+  if constexpr (SCH && !MW && MCPX_NL_SEHOIST) se_tab.load(lane);
   int piv_guess = 0;        // SCHUR: lane k = pivot row of LU step k at the last Newton step
   bool have_guess = false;  // (lu_solve_rows_core)
 #if MCPX_STAMPS
@@ -659,7 +703,8 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
         // (MW: wave 0 forms the rows into Srow for lu_solve_mw)
         const int i = lx ? lane : 0;
         if constexpr (!MW) {
-          schur_form_entries<LDR>(Srow, blk, Fs, sDi, sTy, tol, lane);
+          schur_form_entries<LDR, (bool)MCPX_NL_SCOL>(Srow, blk, Fs, sDi, sTy, tol, lane,
+                                                       MCPX_NL_SEHOIST ? &se_tab : nullptr);
           __syncthreads();
           MCPX_STAMP(1);
           // LU of [S | rr] (oracle lu_solve_x, reciprocal multipliers) with the previous
@@ -670,14 +715,14 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
           // never a pivot row, never updated (lu_solve_rows_core).
           bool miss = true;
           if (have_guess) {
-            miss = !lu2d_solve<n>(Srow, LDR, lane, piv_guess, dz);
+            miss = !lu2d_solve<n, (bool)MCPX_NL_SCOL>(Srow, LDR, lane, piv_guess, dz);
             ok = !miss;
           }
           if (miss) {
             double a[NMAX];
 #pragma unroll
-            for (int j = 0; j < NMAX; ++j) a[j] = (j < n) ? Srow[i * LDR + j] : 0.0;
-            const double rhs = Srow[i * LDR + n];
+            for (int j = 0; j < NMAX; ++j) a[j] = (j < n) ? Srow[MCPX_NL_SCOL ? j * n + i : i * LDR + j] : 0.0;
+            const double rhs = Srow[MCPX_NL_SCOL ? n * n + i : i * LDR + n];
             bool unused;
             ok = lu_solve_rows_core<NMAX, true>(a, rhs, opaque(n), lane, dz, piv_guess, false, unused);
           }
