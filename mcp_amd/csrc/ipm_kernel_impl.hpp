@@ -55,9 +55,10 @@
 #endif
 
 // SCHUR kernels with compile-time n ≤ 16 (C2) keep M in LDS as well (A/B knob): its 2 KB per
-// wave fit beside A at the occupancy those kernels run at.
+// wave fit beside A at the occupancy those kernels run at, and the residual's and the Schur
+// accumulator's M reads stop paying an L2 round trip (C2 +3 to +6 %, ab_c2_lds_m.jsonl).
 #ifndef MCPX_LDS_M
-#define MCPX_LDS_M 0
+#define MCPX_LDS_M 1
 #endif
 
 // kkt and ϵ re-read into SGPRs after each update (A/B knob).
