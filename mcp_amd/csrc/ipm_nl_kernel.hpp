@@ -218,7 +218,9 @@ __device__ __forceinline__ void lu2d_step(double (&acc)[Lu2d<NM>::NJ][Lu2d<NM>::
   constexpr int Jk = K >> 4, Rk = K & 15;
   constexpr bool NX = K + 1 < NM;  // a next pivot to fetch
   constexpr int Jn = (K + 1) >> 4, Rn = (K + 1) & 15, Qn = (K + 1) & 3, Cn = (K + 1) >> 2;
-  __builtin_amdgcn_sched_barrier(0);  // one step at a time: no step's uniform values hoisted ahead
+  // (a sched_barrier here — one step at a time — cost 2.6 %: the scheduler may overlap a step's
+  // tail with the next step's check; the one wave per SIMD has registers to spare,
+  // profiles/r04/ab_c4_sched_barrier.jsonl)
   const int lc = ln & 15;
   {  // the first-max rule over the remaining positions
     const int pkk = __builtin_amdgcn_readlane(pv[Jk], Rk);
