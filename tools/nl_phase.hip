@@ -94,6 +94,23 @@ int main(int argc, char** argv) {
   (void)hipMemcpy(nw.data(), newton, B * 4, hipMemcpyDeviceToHost);
   (void)hipMemcpy(stt.data(), status, B * 4, hipMemcpyDeviceToHost);
   const char* nm[] = {"eval+F+kkt", "schur prep+form", "LU (rest)", "dy/ds+linesearch+update", "LU elimination (2-D)", "2-D LU rejected (count)"};
+  if (NST == 8) {  // the workgroup kernel's diagnostic build: four phases, then the LU's parts
+    const char* nm8[] = {"eval+F+kkt", "schur prep+entries", "LU (all)", "dy/ds+linesearch+update",
+                         "  LU: entries into tiles", "  LU: panel factor", "  LU: panel back + U12", "  LU: trailing (MFMA)"};
+    for (int grp = 0; grp < 2; ++grp) {
+      double tot[8] = {}, steps = 0;
+      int cnt = 0;
+      for (int b = 0; b < B; ++b) {
+        if ((stt[b] != 0) != (grp == 1)) continue;
+        for (int i = 0; i < 8; ++i) tot[i] += st[(size_t)b * 8 + i];
+        steps += nw[b];
+        ++cnt;
+      }
+      printf("[%s] %s: %d instances, %.0f Newton steps\n", kname, grp ? "failed" : "solved", cnt, steps);
+      for (int i = 0; i < 8; ++i) printf("  %-28s %10.0f cyc/step\n", nm8[i], steps ? tot[i] / steps : 0.0);
+    }
+    return 0;
+  }
   for (int grp = 0; grp < 2; ++grp) {  // solved, failed
     double tot[8] = {0, 0, 0, 0, 0, 0, 0, 0}, steps = 0; int cnt = 0, mx = 0;
     for (int b = 0; b < B; ++b) {
