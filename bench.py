@@ -622,8 +622,11 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         full = gather.unpack([shard_range(pl["global_batch"], world, r)[1] for r in range(world)]
                              if pl["scaling"] == "strong" else None)
         assert int(full["status"].numel()) == pl["global_batch"], "gathered batch has the wrong size"
-        mine = full["status"][pl["start"]:pl["start"] + B].to(dev)
-        assert torch.equal(mine, out["status"]), "gathered results differ from this rank's"
+        for k in ("status", "newton_iters", "active_mask", "fail_reason", "x"):  # x by bits (NaN included)
+            mine, own = full[k][pl["start"]:pl["start"] + B].to(dev), out[k]
+            if mine.dtype == torch.float64:
+                mine, own = mine.view(torch.int64), own.view(torch.int64)
+            assert torch.equal(mine, own), f"gathered {k} differs from this rank's"
     if rank != 0:
         return
     G = pl["global_batch"]

@@ -71,7 +71,7 @@ def alloc_host_outputs(B: int, n: int, m: int, trace_len: int = 0) -> dict:
         x=np.zeros((B, n)), y=np.zeros((B, m)), s=np.zeros((B, m)), kkt_error=np.zeros(B),
         eps=np.zeros(B), outer_iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32),
         newton_iters=np.zeros(B, np.int32),
-        active_mask=np.zeros((B, words), np.uint64) if m <= 64 else None,
+        active_mask=np.zeros((B, words), np.uint64),
         alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
         fail_reason=np.zeros(B, np.uint8),
     )
@@ -101,7 +101,7 @@ def solve_batch(family: int, n: int, m: int, theta, *, x0=None, y0=None, s0=None
             x=np.empty((B, n)), y=np.empty((B, m)), s=np.empty((B, m)), kkt_error=np.empty(B),
             eps=np.empty(B), outer_iters=np.empty(B, np.int32), status=np.empty(B, np.int32),
             newton_iters=np.empty(B, np.int32),
-            active_mask=np.empty((B, words), np.uint64) if m <= 64 else None,
+            active_mask=np.empty((B, words), np.uint64),
             alpha_trace=np.full((B, max(trace_len, 0), 2), 254, np.uint8),
             fail_reason=np.empty(B, np.uint8),
         )
@@ -150,7 +150,9 @@ def alloc_device_outputs(B: int, n: int, m: int, device, trace_len: int = 0, new
         kkt_error=torch.empty(B, **f64), eps=torch.empty(B, **f64),
         outer_iters=torch.empty(B, **i32), status=torch.empty(B, **i32),
         newton_iters=torch.empty(B, **i32) if newton else None,
-        active_mask=torch.empty(B, dtype=torch.int64, device=device) if (active and m <= 64) else None,
+        # one uint64 word per instance up to m = 64 (shape (B,)), else (B, ⌈m/64⌉) words
+        active_mask=(torch.empty(B, dtype=torch.int64, device=device) if m <= 64 else
+                     torch.empty(B, (m + 63) // 64, dtype=torch.int64, device=device)) if active else None,
         alpha_trace=torch.full((B, trace_len, 2), 254, dtype=torch.uint8, device=device) if trace_len > 0 else None,
         fail_reason=torch.empty(B, dtype=torch.uint8, device=device),
     )

@@ -230,8 +230,11 @@ class NLSystem:
 
     # ---- which one-wave kernels the module gets (csrc/ipm_nl_kernel.hpp) -------
     def schur_lds_bytes(self) -> int:
+        """MCPX_NL_SCHUR_LDS of csrc/ipm_nl_kernel.hpp: the blocks up to S, the n×(n+1) rows
+        of [S | rr], z / δz / F and the four per-constraint arrays (tests/test_codegen_masks.py
+        evaluates the C macros against these formulas)."""
         n, m = self.n, self.m
-        return 8 * (self.OFF_S + m * n + 3 * (n + 2 * m) + 4 * m)
+        return 8 * (self.OFF_S + n * (n + 1) + 3 * (n + 2 * m) + 4 * m)
 
     def solvers(self) -> dict:
         n, m = self.n, self.m
@@ -503,9 +506,7 @@ class NLSystem:
         text, the kernel headers it includes and the compiler flags (self.key, the
         oracle's cache key, covers the generated text only)."""
         h = hashlib.sha256(self.key.encode())
-        for f in _MODULE_DEPS:
-            h.update(f.encode() + b"\0" + open(os.path.join(CSRC, f), "rb").read())
-        h.update(" ".join(_MODULE_FLAGS).encode())
+        h.update(deps_hash().encode())
         return h.hexdigest()[:24]
 
     def module_path(self) -> str:
@@ -530,8 +531,21 @@ class NLSystem:
             raise RuntimeError(f"hipcc failed on the generated module {src}:\n{r.stderr[-6000:]}")
         _check_hazards(tmp_dir)
         os.replace(tmp, path)
+        with open(os.path.splitext(path)[0] + ".dep", "w") as f:  # what __graft_entry__ prunes by
+            f.write(deps_hash())
         shutil.rmtree(tmp_dir, ignore_errors=True)
         return path
+
+
+def deps_hash() -> str:
+    """Hash of the kernel headers and compiler flags every module is built with: the part of
+    module_key() beyond the generated text.  A code object whose `.dep` record differs was built
+    from other headers and can never be loaded again."""
+    h = hashlib.sha256()
+    for f in _MODULE_DEPS:
+        h.update(f.encode() + b"\0" + open(os.path.join(CSRC, f), "rb").read())
+    h.update(" ".join(_MODULE_FLAGS).encode())
+    return h.hexdigest()[:24]
 
 
 def _check_hazards(tmp_dir: str) -> None:

@@ -701,7 +701,6 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
         }
         __syncthreads();
         // row i of S = (P + tol·I) − Q D⁻¹ R and rr_i = −F_Gi − Σ_k Q_ik ty_k, k ascending
-        // lanes ≥ n hold a copy of row 0: never a pivot row, never updated (lu_solve_rows)
         // (MW: wave 0 forms the rows into Srow for lu_solve_mw)
         const int i = lx ? lane : 0;
         if constexpr (!MW) {
@@ -709,12 +708,14 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
                                                        MCPX_NL_SEHOIST ? &se_tab : nullptr);
           __syncthreads();
           MCPX_STAMP(1);
-          // LU of [S | rr] (oracle lu_solve_x, reciprocal multipliers) with the previous
-          // Newton step's pivot sequence as the guess (the lane-change game keeps it on 86 %
-          // of steps): the 2-D elimination (lu2d_solve) reads the rows in the guessed order;
-          // a missed guess leaves Srow as it was and the register LU with the pivot search
-          // factors its rows.  Bits equal the searched LU.  Lanes ≥ n hold a copy of row 0:
-          // never a pivot row, never updated (lu_solve_rows_core).
+          // Gauss-Jordan with partial pivoting of [S | rr] (oracle lu_solve_x, rcp = 2) with the
+          // previous Newton step's pivot sequence as the guess (the lane-change game keeps it on
+          // 86 % of steps), repaired in place at a step whose guess breaks the first-max rule
+          // (lu2d_fix): the 2-D elimination (lu2d_solve) reads the rows in the guessed order.  A
+          // zero, NaN or out-of-range pivot leaves Srow as it was and the searched Gauss-Jordan
+          // of lu_solve_rows_core (GJ = true) factors its rows.  Bits equal the oracle's rcp = 2
+          // elimination either way.  Lanes ≥ n hold a copy of row 0: the GJ updates every lane
+          // uniformly, so they are updated too, but never a pivot row and never read.
           bool miss = true;
           if (have_guess) {
             miss = !lu2d_solve<n, (bool)MCPX_NL_SCOL>(Srow, LDR, lane, piv_guess, dz);
@@ -946,11 +947,15 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
       args.s[inst * m + k] = zs[n + m + k];
     }
   }
-  if (args.active_mask && m <= 64) {
-    bool act = false;
-    if (lane < m) act = zs[n + imin(lane, MZ - 1)] > zs[n + m + imin(lane, MZ - 1)];
-    const uint64_t bits = ballot(act);
-    if (tid == 0) args.active_mask[inst] = bits;
+  if (args.active_mask) {  // W = ⌈m/64⌉ words (include/mcpx.h): one ballot per word
+#pragma unroll
+    for (int r = 0; r < imax(RM, 1); ++r) {
+      const int k = lane + 64 * r;
+      bool act = false;
+      if (k < m) act = zs[n + imin(k, MZ - 1)] > zs[n + m + imin(k, MZ - 1)];
+      const uint64_t bits = ballot(act);
+      if (tid == 0) args.active_mask[inst * imax(RM, 1) + r] = bits;
+    }
   }
 #if MCPX_STAMPS
   if (tid == 0 && args.stamps)

@@ -774,12 +774,13 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
       else if (i < n + m) a.y[inst * m + (i - n)] = zs[i];
       else a.s[inst * m + (i - n - m)] = zs[i];
     }
-    if (a.active_mask) {  // m ≤ 64 (checked by the host)
-      uint64_t act = 0ull;
-      for (int k = tid; k < m; k += WG)
-        if (zs[n + k] > zs[n + m + k]) act |= 1ull << k;
-      act = wg_or(act, S.sc);
-      if (tid == 0) a.active_mask[inst] = act;
+    if (a.active_mask && tid < 64) {  // W = ⌈m/64⌉ words (include/mcpx.h), wave 0 by ballots
+      const int W = m > 64 ? (m + 63) / 64 : 1;
+      for (int q = 0; q < W; ++q) {
+        const int k = 64 * q + tid, kk = k < m ? k : 0;
+        const uint64_t act = __ballot(k < m && zs[n + kk] > zs[n + m + kk]);
+        if (tid == 0) a.active_mask[inst * W + q] = act;
+      }
     }
     if (tid == 0) {
       a.kkt_error[inst] = kkt;

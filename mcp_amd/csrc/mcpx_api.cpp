@@ -247,6 +247,9 @@ hipError_t launch(int nmax, const mcpx::KernelArgs& a, int64_t nb, hipStream_t s
   }
 }
 
+// uint64 words of one instance's active-set mask: ⌈m/64⌉, at least 1 (include/mcpx.h)
+inline int64_t mask_words(int m) { return m > 64 ? (m + 63) / 64 : 1; }
+
 // Per-instance pointers of chunk [b0, b0 + nb) into the kernel args.
 void set_chunk(mcpx::KernelArgs& a, const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                const double* s0, const mcpx_out* o, int64_t b0) {
@@ -263,7 +266,7 @@ void set_chunk(mcpx::KernelArgs& a, const mcpx_desc* d, const double* theta, con
   a.outer_iters = o->outer_iters + b0;
   a.status = o->status + b0;
   a.newton_iters = o->newton_iters ? o->newton_iters + b0 : nullptr;
-  a.active_mask = o->active_mask ? o->active_mask + b0 : nullptr;
+  a.active_mask = o->active_mask ? o->active_mask + b0 * mask_words(m) : nullptr;
   a.alpha_trace = (o->alpha_trace && o->trace_len > 0) ? o->alpha_trace + b0 * (int64_t)o->trace_len * 2 : nullptr;
   a.trace_len = o->alpha_trace ? o->trace_len : 0;
   a.fail_reason = o->fail_reason ? o->fail_reason + b0 : nullptr;
@@ -514,7 +517,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   bool wg = false, mw = false;
   if ((rc = prepare(d, prm, &a, &nmax, mod, &wg, &mw))) return rc;
   const int n = d->n, m = d->m;
-  if (m > 64 && o->active_mask) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
+  const int64_t W = mask_words(m);
   PipeLease lease;
   if ((rc = lease.acquire(dev))) return rc;
   Pipe* P = lease.p;
@@ -547,7 +550,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   HIP_TRY(kkt.alloc(nb, cs)); HIP_TRY(eps.alloc(nb, cs)); HIP_TRY(outer.alloc(nb, cs));
   HIP_TRY(status.alloc(nb, cs));
   if (o->newton_iters) HIP_TRY(newton.alloc(nb, cs));
-  if (o->active_mask) HIP_TRY(am.alloc(nb, cs));
+  if (o->active_mask) HIP_TRY(am.alloc((size_t)nb * W, cs));
   if (o->fail_reason) HIP_TRY(fr.alloc(nb, cs));
   const bool want_tr = o->alpha_trace && o->trace_len > 0;
   if (want_tr) {
@@ -570,7 +573,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
     mcpx_out od{};
     od.x = x.p + c0 * n; od.y = y.p + c0 * m; od.s = s.p + c0 * m; od.kkt_error = kkt.p + c0; od.eps = eps.p + c0;
     od.outer_iters = outer.p + c0; od.status = status.p + c0; od.newton_iters = newton.p ? newton.p + c0 : nullptr;
-    od.active_mask = am.p ? am.p + c0 : nullptr;
+    od.active_mask = am.p ? am.p + c0 * W : nullptr;
     od.alpha_trace = want_tr ? tr.p + c0 * (int64_t)o->trace_len * 2 : nullptr;
     od.trace_len = want_tr ? o->trace_len : 0;
     od.fail_reason = fr.p ? fr.p + c0 : nullptr;
@@ -592,7 +595,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   HIP_TRY(back(o->outer_iters + b0, outer.p, sizeof(int32_t) * nb));
   HIP_TRY(back(o->status + b0, status.p, sizeof(int32_t) * nb));
   if (o->newton_iters) HIP_TRY(back(o->newton_iters + b0, newton.p, sizeof(int32_t) * nb));
-  if (o->active_mask) HIP_TRY(back(o->active_mask + b0, am.p, sizeof(uint64_t) * nb));
+  if (o->active_mask) HIP_TRY(back(o->active_mask + b0 * W, am.p, sizeof(uint64_t) * nb * W));
   if (want_tr) HIP_TRY(back(o->alpha_trace + b0 * o->trace_len * 2, tr.p, (size_t)nb * o->trace_len * 2));
   if (o->fail_reason) HIP_TRY(back(o->fail_reason + b0, fr.p, (size_t)nb));
   return MCPX_OK;
@@ -935,7 +938,6 @@ int solve_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta,
   if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
   if (d->batch == 0) return MCPX_OK;
   if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
-  if (o->active_mask && d->m > 64) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
   int dev = 0;
   if ((rc = current_device(&dev))) return rc;
   return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod, wg, mw);
@@ -958,7 +960,6 @@ int solve_vjp_device_impl(const mcpx_desc* d, const double* theta, const double*
   if (!ct) return fail(MCPX_EINVAL, "the cotangent must be non-NULL");
   if (d->batch == 0) return MCPX_OK;
   if (!theta || !dtheta) return fail(MCPX_EINVAL, "theta and dtheta must be non-NULL");
-  if (o->active_mask && d->m > 64) return fail(MCPX_EUNSUPPORTED, "active_mask needs m <= 64");
   int dev = 0;
   if ((rc = current_device(&dev))) return rc;
   const hipStream_t st = (hipStream_t)stream;

@@ -6,9 +6,11 @@ during the solve.  The only collective is the final solution collection
 (north_star: "RCCL all-gather over xGMI only for the final solution
 collection"): every rank writes its per-instance results into one packed fp64
 record buffer (x | y | s | kkt_error | ϵ) and one int32 buffer
-(outer_iters | status | newton_iters), and two all-gathers (RCCL over xGMI with
-the "nccl" backend; gloo works the same way on CPU, which the tests use)
-deliver the whole batch to every rank.
+(active_mask words | outer_iters | status | newton_iters | fail_reason bytes),
+and two all-gathers (RCCL over xGMI with the "nccl" backend; gloo works the
+same way on CPU, which the tests use) deliver the whole batch to every rank —
+the integer active-set indices and the per-instance failure reasons included
+(north_star: "integer active-set indices bit-exact").
 
 Shards may differ by one instance (``shard_range``: ⌊B/G⌋, +1 for the first
 B mod G ranks).  A collective needs equal buffer sizes, so every rank's packed
@@ -38,6 +40,20 @@ _FP_FIELDS = (("x", "n"), ("y", "m"), ("s", "m"), ("kkt_error", 1), ("eps", 1))
 _INT_FIELDS = ("outer_iters", "status", "newton_iters")
 
 
+def mask_words(m: int) -> int:
+    """uint64 words of one instance's active-set mask (include/mcpx.h: ⌈m/64⌉, at least 1)."""
+    return max(1, (int(m) + 63) // 64)
+
+
+def irec_len(cap: int, m: int) -> int:
+    """int32 entries of the integer record for `cap` instances: the mask words (two int32 each,
+    first, so the uint64 view is 8-byte aligned), three counters, ⌈cap/4⌉ words of fail_reason
+    bytes; rounded up to even, so that every rank's block of the gathered buffer starts 8-byte
+    aligned."""
+    L = cap * (2 * mask_words(m) + 3) + (cap + 3) // 4
+    return L + (L & 1)
+
+
 @dataclass
 class PackedResults:
     """Per-instance outputs laid out for a single collective each.
@@ -47,7 +63,8 @@ class PackedResults:
     same size)."""
 
     rec: "object"   # fp64 [cap * (n + 2m + 2)]: x (cap×n) | y (cap×m) | s (cap×m) | kkt (cap) | ϵ (cap)
-    irec: "object"  # int32 [3 cap]: outer_iters | status | newton_iters
+    irec: "object"  # int32 [irec_len(cap, m)]: active_mask (cap×words uint64) | outer_iters | status |
+    #                 newton_iters | fail_reason (cap bytes)
     B: int
     n: int
     m: int
@@ -71,11 +88,7 @@ class PackedResults:
             w = self._width(w)
             out[k] = self.rec[o:o + B * w].view(B, w) if k in ("x", "y", "s") else self.rec[o:o + B]
             o += cap * w
-        for i, k in enumerate(_INT_FIELDS):
-            out[k] = self.irec[i * cap:i * cap + B]
-        out["active_mask"] = None
-        out["alpha_trace"] = None
-        return out
+        return dict(out, **_int_views(self.irec, B, cap, self.m), alpha_trace=None)
 
 
 def alloc_packed(B: int, n: int, m: int, device, capacity: int | None = None) -> PackedResults:
@@ -83,7 +96,21 @@ def alloc_packed(B: int, n: int, m: int, device, capacity: int | None = None) ->
 
     cap = B if capacity is None else int(capacity)
     return PackedResults(torch.empty(max(cap, 1) * (n + 2 * m + 2), dtype=torch.float64, device=device),
-                         torch.empty(3 * max(cap, 1), dtype=torch.int32, device=device), B, n, m, cap)
+                         torch.zeros(irec_len(max(cap, 1), m), dtype=torch.int32, device=device), B, n, m, cap)
+
+
+def _int_views(irec, B: int, cap: int, m: int) -> dict:
+    """The first B instances of each integer field of one rank's int32 record."""
+    import torch
+
+    W = mask_words(m)
+    o = 2 * W * cap
+    out = {"active_mask": irec[:2 * W * B].view(torch.int64).view(B, W)}
+    for i, k in enumerate(_INT_FIELDS):
+        out[k] = irec[o + i * cap:o + i * cap + B]
+    o += 3 * cap
+    out["fail_reason"] = irec[o:o + (cap + 3) // 4].view(torch.uint8)[:B]
+    return out
 
 
 class Gatherer:
@@ -142,6 +169,7 @@ class Gatherer:
             cat = torch.cat(parts, 0)
             out[k] = cat if k in ("x", "y", "s") else cat.reshape(-1)
             o += cap * w
-        for i, k in enumerate(_INT_FIELDS):
-            out[k] = torch.cat([irecs[r, i * cap:i * cap + counts[r]] for r in range(self.world)])
+        parts = [_int_views(irecs[r], counts[r], cap, m) for r in range(self.world)]
+        for k in _INT_FIELDS + ("active_mask", "fail_reason"):
+            out[k] = torch.cat([p[k] for p in parts])
         return out

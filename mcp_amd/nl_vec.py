@@ -270,7 +270,15 @@ def build(nl, reps, red, entries, names) -> Program | None:
     prog = Program(nl.n, nl.m, nl.p, nl.size, b.chains, outputs)
     if prog.ev_size * 8 >= 65536:
         return None
+    steps, _, _ = prog.tables()
+    # the one-wave kernel keeps one operand word per term step and one destination per slot in
+    # VGPRs for the whole solve (eval_vec): beyond these caps they would spill to scratch
+    if sum(steps) > MAX_WORDS or len(steps) > MAX_SLOTS:
+        return None
     return prog
+
+
+MAX_WORDS, MAX_SLOTS = 64, 32  # VGPR budget of eval_vec's word and destination tables
 
 
 def emit(prog: Program) -> list:

@@ -15,10 +15,11 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mcp_amd.distributed import Gatherer, alloc_packed, shard_capacity, shard_range
+from mcp_amd.distributed import Gatherer, alloc_packed, irec_len, shard_capacity, shard_range
 from mcp_amd.qp_benchmark import generate_random_parameter
 
 N_, M_, B_TOTAL = 16, 8, 25  # ragged: 13 + 12 instances
+FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters", "active_mask", "fail_reason")
 
 
 def _free_port():
@@ -36,20 +37,24 @@ def _worker(rank, world, port, ret):
         from oracle import coracle
 
         th_all = generate_random_parameter(np.random.default_rng(3), N_, M_, 0.0, batch=B_TOTAL)
+        th_all[::7, N_ * N_:N_ * N_ + N_ * M_] = 0.0  # A = 0 with b > 0: infeasible, failing instances
         start, cnt = shard_range(len(th_all), world, rank)
         packed = alloc_packed(cnt, N_, M_, "cpu", capacity=shard_capacity(B_TOTAL, world))
         out = packed.views()
         r = coracle.solve_batch(0, N_, M_, th_all[start:start + cnt], tol=1e-6, linear_solver="schur")
-        for k in ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters"):
+        r["active_mask"] = r["active_mask"].view(np.int64)  # the packed record's int64 view
+        for k in FIELDS:
             out[k].copy_(torch.from_numpy(np.ascontiguousarray(r[k]).reshape(out[k].shape)))
         g = Gatherer(packed)
         g()
         full = g.unpack([shard_range(B_TOTAL, world, r)[1] for r in range(world)])
         if rank == 0:
             ref = coracle.solve_batch(0, N_, M_, th_all, tol=1e-6, linear_solver="schur")
-            ok = all(np.array_equal(full[k].numpy(), ref[k].reshape(full[k].shape))
-                     for k in ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters"))
-            ret.put(ok)
+            ref["active_mask"] = ref["active_mask"].view(np.int64)
+            bad = [k for k in FIELDS if not np.array_equal(full[k].numpy(), ref[k].reshape(full[k].shape))]
+            # the integer outputs must carry information, not agree by being all zero
+            informative = (ref["active_mask"] != 0).any() and (ref["fail_reason"] != 0).any()
+            ret.put((bad, bool(informative)))
     finally:
         dist.destroy_process_group()
 
@@ -74,7 +79,21 @@ def test_gloo_world2_sharded_solve_and_gather(oracle_lib):
     for p in procs:
         p.join(timeout=180)
         assert p.exitcode == 0
-    assert ret.get(timeout=10) is True
+    bad, informative = ret.get(timeout=10)
+    assert bad == [] and informative
+
+
+def test_packed_integer_fields_with_wide_masks():
+    """m > 64: ⌈m/64⌉ mask words per instance; fail_reason bytes after the counters."""
+    p = alloc_packed(3, 2, 130, "cpu", capacity=4)
+    v = p.views()
+    assert v["active_mask"].shape == (3, 3) and v["active_mask"].dtype == torch.int64
+    assert v["fail_reason"].shape == (3,) and v["fail_reason"].dtype == torch.uint8
+    v["active_mask"].copy_(torch.arange(9).view(3, 3))
+    v["status"].fill_(1)
+    v["fail_reason"].copy_(torch.tensor([1, 2, 4], dtype=torch.uint8))
+    assert p.irec[:18].view(torch.int64).tolist() == list(range(9))
+    assert p.irec.numel() % 2 == 0
 
 
 def test_packed_views_with_padding():
@@ -82,7 +101,7 @@ def test_packed_views_with_padding():
     p = alloc_packed(3, 4, 2, "cpu", capacity=5)
     v = p.views()
     assert v["x"].shape == (3, 4) and v["y"].shape == (3, 2) and v["status"].shape == (3,)
-    assert p.rec.numel() == 5 * (4 + 2 * 2 + 2) and p.irec.numel() == 15
+    assert p.rec.numel() == 5 * (4 + 2 * 2 + 2) and p.irec.numel() == irec_len(5, 2) == 28
     v["s"].fill_(7.0)
     assert float(p.rec[5 * 4 + 5 * 2:5 * 4 + 5 * 2 + 6].sum()) == 42.0  # s block starts after cap·(n + m)
     with pytest.raises(ValueError):
