@@ -45,7 +45,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (MI355X_MICROAR
 HBM_PEAK_GBS = 8000.0
 XCDS, SIMDS = 8, 256 * 4  # MI355X: 8 XCDs, 256 CUs × 4 SIMDs
 # rocprofv3 evidence of this round's kernels (tools/gpu_profile.sh + tools/prof_summary.py)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
 DEFAULT_GLOBAL = {"c3": 65536, "c5": 4096, "c4": 1024}
 QP_FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters")
 C4_FIELDS = QP_FIELDS
@@ -79,15 +79,29 @@ def executed_flops(n: int, m: int, linear_solver: str) -> float:
     return resid + lu_flops(solve_dim(n, m, linear_solver))
 
 
-def executed_flops_nl(nl, linear_solver: str) -> float:
+def executed_flops_nl(nl, linear_solver: str, band: bool = False) -> float:
     """Same for a generated nonlinear module: the linear solve only (the generated G/H
     evaluation is not counted) — schur: R·D⁻¹ (m·n products), S from Q's structural
-    nonzeros (2n per term), rr and δy over the Q / R patterns, LU of S."""
+    nonzeros (2n per term), rr and δy over the Q / R patterns, LU of S; with the band kernel
+    (csrc/ipm_nl_band.hpp) the LU of S is the band elimination: per step one reciprocal, NS
+    multipliers and the NS × WC window update (2 flops each), and the back substitution's WC
+    updates per row."""
     n, m = nl.n, nl.m
     if linear_solver != "schur":
         return lu_flops(solve_dim(n, m, linear_solver))
     (qp, qi), (rp, ri) = nl.structure()
-    return m * n + 2.0 * n * len(qi) + 2.0 * len(qi) + 2.0 * len(ri) + lu_flops(n)
+    form = m * n + 2.0 * n * len(qi) + 2.0 * len(qi) + 2.0 * len(ri)
+    if band:
+        b = nl.band
+        return form + n * (1.0 + b.ns + 2.0 * b.ns * b.wc + 2.0 * b.wc)
+    return form + lu_flops(n)
+
+
+def band_kernel_runs(nl, linear_solver: str, kernel: str) -> bool:
+    """Whether the C ABI runs a module's band SCHUR kernel (mcpx_api.cpp prepare: forced, or
+    AUTO when the module prefers it or has no one-wave SCHUR kernel)."""
+    return linear_solver == "schur" and nl.band_can and (
+        kernel == "band" or (kernel == "auto" and (nl.band_auto or not nl.solvers()["schur"])))
 
 
 def one_wave(n: int, m: int, linear_solver: str) -> bool:
@@ -199,6 +213,9 @@ def parse(argv=None):
     ap.add_argument("--sparsity", type=float, default=0.0)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--linear-solver", default="schur", choices=["reduced", "dense", "schur"])
+    ap.add_argument("--family", default="qp", choices=["qp", "affine"],
+                    help="affine: the same QPs handed over as affine-family data (P = M, Q = -A^T, R = A, S = 0, "
+                         "g = -phi, h = -b), the layout the Julia shim's affine_parameters produces (INTEGRATION.md)")
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="instances in the CPU-baseline sample (-1 = 2048 per thread, 0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use (nproc)")
@@ -211,7 +228,7 @@ def parse(argv=None):
                          "mcpx_vjp_batch_device) instead of mcpx_solve_vjp_batch_device")
     ap.add_argument("--gather", action="store_true",
                     help="run the RCCL result collection even at world size 1 (rehearsal under torchrun)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "workgroup", "multiwave"],
+    ap.add_argument("--kernel", default="auto", choices=["auto", "wave", "workgroup", "multiwave", "band"],
                     help="with --lane-change: the generated module's kernel (mcpx_params.kernel)")
     ap.add_argument("--lane-change", type=int, default=0, metavar="T",
                     help="BASELINE C4: each step solves lane-change games of horizon T (generated "
@@ -263,7 +280,7 @@ def launch_ranks(nranks: int, script: str, argv, have_devices: int | None = None
 
 
 def evidence(name: str, cfg: dict) -> dict:
-    """The committed rocprofv3 summaries of this configuration (profiles/r04/
+    """The committed rocprofv3 summaries of this configuration (profiles/r05/
     trace_<name>.json, pmc_<name>.json; tools/prof_summary.py), if they were taken on
     exactly this configuration and this build of libmcpx.so; else {}."""
     from mcp_amd.build import built_hash
@@ -466,15 +483,17 @@ def main_lane_change(a, world, rank, local, dist, pl):
     key = f"c4{'s' if a.sens else ''}_lane_t{a.lane_change}_b{B}"
     ev = evidence(key, cfg)
     mw = ls == "schur" and a.kernel == "multiwave" and module.has_schur_mw
-    kernel = "mcpx_nl_solve_" + ls + ("_mw" if mw else ("" if mcp.nl.solvers()[ls] and a.kernel != "workgroup"
-                                                         else "_wg"))
-    rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops_nl(mcp.nl, ls),
+    bandk = band_kernel_runs(mcp.nl, ls, a.kernel)
+    kernel = "mcpx_nl_solve_band" if bandk else "mcpx_nl_solve_" + ls + (
+        "_mw" if mw else ("" if mcp.nl.solvers()[ls] and a.kernel != "workgroup" else "_wg"))
+    rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops_nl(mcp.nl, ls, bandk),
                   B * 8.0 * (mcp.nl.p + n + 2 * m + 2) + 12.0 * B, ev, kernel, roofline_bound(ev, kern_ms, "latency"),
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system per Newton step) "
                   f"x rank 0's own Newton counts / HIP-event kernel time; executed = the linear solve the kernel "
-                  f"performs ({ls}: LU of dim {solve_dim(n, m, ls)}" + (" + the Schur complement from Q's structural "
-                  "nonzeros" if ls == "schur" else "") + "); bound: per-wave latency (PMC: waves stall on LDS/VALU "
-                  "dependencies, DESIGN.md §4)")
+                  f"performs ({ls}: " + (f"band LU of the reordered {n}x{n} S, window {mcp.nl.band.ns}x"
+                  f"{mcp.nl.band.wc}" if bandk else f"LU of dim {solve_dim(n, m, ls)}") +
+                  (" + the Schur complement from Q's structural nonzeros" if ls == "schur" else "") +
+                  "); bound: per-wave latency (PMC: waves stall on LDS/VALU dependencies, DESIGN.md §4)")
     res = {
         "metric": ("MCP solve+VJP/sec (lane-change trajectory game, generated nonlinear module, rrule pullback of "
                    "x₁ as examples/utils.jl:236-261)" if a.sens else
@@ -535,6 +554,13 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     n, m, B = a.n, a.m, pl["count"]
     N = n + 2 * m
     theta_host = generate_global_slice(a.seed, n, m, a.sparsity, pl["start"], B)
+    fam = 1 if a.family == "affine" else 0  # MCPX_FAMILY_AFFINE / _QP
+    if fam:
+        if a.sens:
+            raise SystemExit("bench.py: --family affine has no --sens (the fused pullback is the QP family's)")
+        from mcp_amd.qp_benchmark import affine_embedding
+
+        theta_host = affine_embedding(theta_host, n, m)
     theta = torch.from_numpy(theta_host).to(dev)
     # outputs written straight into one packed fp64 record buffer + one int32 buffer
     # (x | y | s | kkt | ϵ and outer | status | newton), so the collection is 2 all-gathers
@@ -566,7 +592,7 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
             solve_vjp_batch_device(0, n, m, theta, out, ct=(2.0, 2.0, 0.0), dtheta=dtheta, status=vstat,
                                    tol=a.tol, linear_solver=a.linear_solver, stream=stream)
         else:
-            solve_batch_device(0, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
+            solve_batch_device(fam, n, m, theta, out, tol=a.tol, linear_solver=a.linear_solver, stream=stream)
         if evs:
             evs[0][1].record(stream)
         if a.sens and not fused:
@@ -590,11 +616,11 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         from mcp_amd.batch import alloc_host_outputs, pinned
 
         def host_runs(out=None):
-            solve_batch(0, n, m, theta_host[:1024], tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
+            solve_batch(fam, n, m, theta_host[:1024], tol=a.tol, linear_solver=a.linear_solver, num_devices=1)
             runs = []
             for _ in range(a.host_runs):
                 t1 = time.perf_counter()
-                solve_batch(0, n, m, theta_host, tol=a.tol, linear_solver=a.linear_solver, num_devices=1, out=out)
+                solve_batch(fam, n, m, theta_host, tol=a.tol, linear_solver=a.linear_solver, num_devices=1, out=out)
                 runs.append(time.perf_counter() - t1)
             return runs
 
@@ -635,8 +661,11 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     cfg = {"mode": ("c5" if fused else "c5u") if a.sens else "c3", "n": n, "m": m, "batch_per_gpu": B, "linear_solver": ls,
            "sparsity": a.sparsity}
     key = f"{cfg['mode']}_n{n}_m{m}_b{B}_{ls}"
+    if fam:
+        cfg["family"] = "affine"
+        key += "_affine"
     ev = evidence(key, cfg)
-    p = n * n + m * n + m + n
+    p = theta_host.shape[1]
     rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
                   B * (8.0 * (p + n + 2 * m + 2) + 12.0), ev,
                   "ipm_solve_kernel" if one_wave(n, m, ls) else "ipm_wg_kernel_t",
@@ -664,10 +693,12 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
         "config": {"workload": (f"BASELINE {'C5' if a.sens else ('C2' if (n, m) == (16, 8) else 'C3')}: random dense "
                                 f"QP-KKT n={n} m={m} (KKT dim {N}), "
                                 f"fp64, global batch {G} ({B} on rank 0), tol={a.tol:g}"
+                                + (", passed as the affine family (P=M, Q=-A^T, R=A, S=0, g=-phi, h=-b: the "
+                                   "Julia shim's layout)" if fam else "")
                                 + ((", solve + rrule pullback of f = Σx²+Σy² "
                                     + ("fused in one kernel" if fused else "(solve, then VJP kernel)"))
                                    if a.sens else "")),
-                   "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "solve_dim": NS,
+                   "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "solve_dim": NS, "family": a.family,
                    "batch_per_gpu": B, "global_batch": G, "sparsity": a.sparsity,
                    "parallelism": f"dp{world} (instance shards, RCCL all-gather of results)" if distributed
                    else "dp1"},
@@ -707,7 +738,7 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
 
         coracle.build()
         th = a.cpu_threads or host_cpus()["nproc"]
-        cb = cpu_baseline(lambda k, t: coracle.solve_batch(0, n, m, theta_host[:k], tol=a.tol, nthreads=t,
+        cb = cpu_baseline(lambda k, t: coracle.solve_batch(fam, n, m, theta_host[:k], tol=a.tol, nthreads=t,
                                                            linear_solver=ls),
                           B, a, th, "C oracle (oracle/ipm_oracle.c, same algorithm and linear solver)")
         r = cb.pop("_result")
@@ -724,7 +755,7 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
                                                  {"dtheta": rd, "status": rs}, ("dtheta", "status"), kv,
                                                  "oracle_vjp_batch on the GPU's solutions")
         res["cpu_baseline"] = cb
-    if world == 1 and not a.sens:
+    if world == 1 and not a.sens and not fam:
         res["parity_fixtures"] = fixture_parity()
     print(json.dumps(res), flush=True)
 

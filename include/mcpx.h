@@ -97,11 +97,17 @@ extern "C" {
  *  MCPX_KERNEL_MULTIWAVE  generated modules, SCHUR: one 4-wave workgroup per
  *                         instance, S in LDS, the LU's columns split over the waves
  *                         (module kernel-mask bit MCPX_MODULE_SCHUR_MW); same bits,
- *                         opt-in (slower than one wave on the lane-change game). */
+ *                         opt-in (slower than one wave on the lane-change game);
+ *  MCPX_KERNEL_BAND       generated modules, SCHUR: one wave per instance, the band LU
+ *                         of the symmetrically reordered Schur complement (module bit
+ *                         MCPX_MODULE_BAND; the oracle's lu_band_solve).  AUTO takes it
+ *                         when the module prefers it (bit MCPX_MODULE_BAND_AUTO) or has
+ *                         no one-wave SCHUR kernel. */
 #define MCPX_KERNEL_AUTO 0
 #define MCPX_KERNEL_WAVE 1
 #define MCPX_KERNEL_WORKGROUP 2
 #define MCPX_KERNEL_MULTIWAVE 3
+#define MCPX_KERNEL_BAND 4
 /* largest max_inner_iters (ϵ-schedule table length) */
 #define MCPX_MAX_INNER_ITERS 128
 /* largest number of line-search trials (α = decayᵉ, e = 0..E) */
@@ -115,15 +121,19 @@ extern "C" {
  *                         Schur complement (default; N ≤ 64 means n + m ≤ 64);
  *  MCPX_LINSOLVE_DENSE    dense LU with partial pivoting of the full
  *                         (n+2m)-dim system (n + 2m ≤ 64);
- *  MCPX_LINSOLVE_SCHUR    ∂H/∂y = 0 (QP family; generated modules without an
- *                         ∂H/∂y block): after the slack block, the now-diagonal
- *                         y block is eliminated as well, leaving the n×n Schur
- *                         complement S = (M + tol·I) + Aᵀ D⁻¹ A (QP: formed on
- *                         the matrix cores, fp64 MFMA).  QP with M exactly
- *                         symmetric: S is solved by pivot-free Gauss-Jordan
- *                         while every pivot is > 0 (S SPD), and by dense LU with
- *                         partial pivoting otherwise — the oracle takes the same
- *                         branch (gj_spd_solve / lu_solve); modules: dense LU with
+ *  MCPX_LINSOLVE_SCHUR    ∂H/∂y = 0 (QP family; affine family, whose S block is
+ *                         then NOT read — ∂H/∂y is taken as 0; generated modules
+ *                         without an ∂H/∂y block): after the slack block, the
+ *                         now-diagonal y block is eliminated as well, leaving the
+ *                         n×n Schur complement S = (M + tol·I) + Aᵀ D⁻¹ A (affine:
+ *                         (P + tol·I) − Q D⁻¹ R; both formed on the matrix cores,
+ *                         fp64 MFMA).  M (affine: P) exactly symmetric (affine:
+ *                         and −Q = Rᵀ exactly): S is solved by pivot-free
+ *                         Gauss-Jordan while every pivot is > 0 (S SPD), and by
+ *                         dense LU with partial pivoting otherwise — the oracle
+ *                         takes the same branch (gj_spd_solve / lu_solve); a QP
+ *                         passed as affine (P = M, Q = −Aᵀ, R = A, g = −ϕ, h = −b)
+ *                         gives the QP solve's bits.  Modules: dense LU with
  *                         partial pivoting.  One wave: n + m ≤ 64. */
 #define MCPX_LINSOLVE_REDUCED 0
 #define MCPX_LINSOLVE_DENSE 1
@@ -306,14 +316,17 @@ int mcpx_jvp_batch_device(const mcpx_desc* desc, const double* theta, const doub
  * one-wave MCPX_LINSOLVE_SCHUR (∂H/∂y ≡ 0, n ≤ 64, m ≤ 128), _REDUCED
  * (n + m ≤ 64), _DENSE (n + 2m ≤ 64), and workgroup-per-instance kernels of
  * each of them (SCHUR: ∂H/∂y ≡ 0) whose LDS footprint fits
- * (e.g. the lane change at T = 10: n = 200, m = 250, KKT dimension 700);
- * another linear_solver is MCPX_EUNSUPPORTED.
+ * (e.g. the lane change at T = 10: n = 200, m = 250, KKT dimension 700), and
+ * the one-wave band SCHUR kernel when the reordered Schur complement has a
+ * narrow band (MCPX_KERNEL_BAND); another linear_solver is MCPX_EUNSUPPORTED.
  */
 typedef struct mcpx_module mcpx_module;
 /* Sensitivity kernels of a module (bits of the mcpx_module_dims kernel mask) */
 #define MCPX_MODULE_VJP 6
 #define MCPX_MODULE_JVP 7
 #define MCPX_MODULE_SCHUR_MW 8  /* the 4-wave SCHUR solve kernel (MCPX_KERNEL_MULTIWAVE) */
+#define MCPX_MODULE_BAND 9       /* the band SCHUR solve kernel (MCPX_KERNEL_BAND) */
+#define MCPX_MODULE_BAND_AUTO 10 /* MCPX_KERNEL_AUTO prefers the band kernel */
 /* Loads the code object at `path` on the current device (other devices load
  * it on first use).  No usable GPU: MCPX_ENODEV. */
 int mcpx_module_load(const char* path, mcpx_module** mod);

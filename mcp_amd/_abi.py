@@ -21,11 +21,13 @@ FAMILY_NONLINEAR = 2  # generated device code per problem (mcp_amd/codegen.py)
 
 MAX_KKT_DIM = 64
 MAX_WG_KKT_DIM = 768  # MCPX_MAX_WG_KKT_DIM: workgroup-per-instance kernels (QP / affine)
-KERNEL_AUTO, KERNEL_WAVE, KERNEL_WORKGROUP, KERNEL_MULTIWAVE = 0, 1, 2, 3
-KERNELS = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "workgroup": KERNEL_WORKGROUP, "multiwave": KERNEL_MULTIWAVE}
+KERNEL_AUTO, KERNEL_WAVE, KERNEL_WORKGROUP, KERNEL_MULTIWAVE, KERNEL_BAND = 0, 1, 2, 3, 4
+KERNELS = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "workgroup": KERNEL_WORKGROUP, "multiwave": KERNEL_MULTIWAVE,
+           "band": KERNEL_BAND}
 JVP_RHS = 8  # MCPX_JVP_RHS: partials per factorisation of the JVP kernel
 MODULE_VJP, MODULE_JVP = 6, 7  # MCPX_MODULE_VJP / _JVP: sensitivity-kernel bits of a module's kernel mask
 MODULE_SCHUR_MW = 8  # MCPX_MODULE_SCHUR_MW: the 4-wave SCHUR solve kernel
+MODULE_BAND, MODULE_BAND_AUTO = 9, 10  # MCPX_MODULE_BAND / _BAND_AUTO: the band SCHUR kernel
 
 LINSOLVE_REDUCED = 0
 LINSOLVE_DENSE = 1

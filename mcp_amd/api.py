@@ -370,6 +370,7 @@ class PrimalDualMCP:
         zs = xs + ys
         self.nl = None
         self._module = None
+        self.h_independent_of_y = False
         try:
             if (backend_options or {}).get("family") == "nonlinear":  # force the generated-code path
                 raise NotAffineError("nonlinear family requested through backend_options")
@@ -386,7 +387,10 @@ class PrimalDualMCP:
         Q = [[CG[i][n + k] for k in range(m)] for i in range(n)]
         R = [[CH[k][j] for j in range(n)] for k in range(m)]
         S = [[CH[k][n + l] for l in range(m)] for k in range(m)]
-        is_qp = (all(sp.expand(S[k][l]) == 0 for k in range(m) for l in range(m))
+        # ∂H/∂y ≡ 0: the SCHUR elimination applies (QP family, or the affine family's S block
+        # structurally zero — include/mcpx.h MCPX_LINSOLVE_SCHUR)
+        self.h_independent_of_y = all(sp.expand(S[k][l]) == 0 for k in range(m) for l in range(m))
+        is_qp = (self.h_independent_of_y
                  and all(sp.expand(Q[i][k] + R[k][i]) == 0 for i in range(n) for k in range(m)))
         colmajor = lambda Mx, r, c: [Mx[i][j] for j in range(c) for i in range(r)]
         if is_qp:
@@ -541,10 +545,15 @@ def _linear_solver(mcp: PrimalDualMCP, linear_solve_algorithm) -> str:
     if linear_solve_algorithm is None:
         if mcp.family == _abi.FAMILY_NONLINEAR:
             return mcp.nl.default_solver()
-        return "schur" if mcp.family == _abi.FAMILY_QP else "reduced"
+        # the MFMA Schur-complement kernel wherever it applies (∂H/∂y ≡ 0, one wave: n + m ≤ 64)
+        one_wave = mcp.unconstrained_dimension + mcp.constrained_dimension <= _abi.MAX_KKT_DIM
+        return "schur" if mcp.h_independent_of_y and one_wave else "reduced"
     if isinstance(linear_solve_algorithm, str):
         if linear_solve_algorithm not in _abi.LINEAR_SOLVERS:
             raise ValueError(f"linear_solve_algorithm must be one of {sorted(_abi.LINEAR_SOLVERS)}")
+        if (linear_solve_algorithm == "schur" and mcp.family == _abi.FAMILY_AFFINE
+                and not mcp.h_independent_of_y):
+            raise ValueError("linear_solve_algorithm='schur' needs ∂H/∂y ≡ 0 (this MCP's H depends on y)")
         return linear_solve_algorithm
     raise TypeError("linear_solve_algorithm: 'reduced' | 'dense' | 'schur' (the kernels' exact eliminations of "
                     "the regularised Newton system; the reference's LinearSolve.jl algorithm objects do not apply)")

@@ -73,14 +73,18 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 Z_VOLATILE_ABOVE = int(os.environ.get("MCPX_NL_Z_VOLATILE_ABOVE", "128"))
 ARCH = "gfx950"
 # bump when the generated text or csrc/ipm_nl_kernel.hpp changes meaning (part of the cache key)
-GEN_VERSION = 7
+GEN_VERSION = 8
 EVAL_PARTS = 4  # mcpx_nl_eval_p0..p3: the generated eval split over the 4-wave SCHUR kernel
 _MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function",
                  "-mllvm", "-amdgpu-mfma-vgpr-form=1")
-_MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "ipm_wg.h",
+_MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_nl_band.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "ipm_wg.h",
                 "ipm_wg_impl.hpp", "lu_vr.hpp", "sens_wg_impl.hpp", "sens_kernel.h", "../../include/mcpx.h")
 WG_LDS_LIMIT = 160 * 1024 - 2048  # MCPX_NL_WG_LIMIT of csrc/ipm_nl_kernel.hpp
 LDS_LIMIT = 160 * 1024 - 2048  # bytes of static LDS one workgroup may declare on gfx950 (minus headroom)
+# band kernel (csrc/ipm_nl_band.hpp): four instances per CU (the C4 batch of 1,024 games on 256
+# CUs) need ≤ 40 KB of LDS each
+BAND_LDS_LIMIT = 40 * 1024
+BAND_KERNEL = True  # the band kernel is compiled into modules (csrc/ipm_nl_band.hpp)
 
 _FUNCS = {  # sympy function → C name (both libm and HIP device math)
     "sin": "sin", "cos": "cos", "tan": "tan", "exp": "exp", "log": "log", "tanh": "tanh",
@@ -410,6 +414,7 @@ class NLSystem:
 
         self.vec = (nl_vec.build(self, cse["reps"], cse["red"], self.var_entries + self.residuals, cse["names"])
                     if cse else None)
+        band_lines = self._emit_band()
         evt = self._block(self.theta_entries, with_z=True, out="dth")
         evp = self._block_parts(self.var_entries + self.residuals, True, EVAL_PARTS)
         parts = []
@@ -458,6 +463,7 @@ class NLSystem:
             arr("mcpx_nl_tr_ptr", trp),
             arr("mcpx_nl_tr_idx", tri),
             *(nl_vec.emit(self.vec) if self.vec is not None else []),
+            *band_lines,
             "MCPX_NL_FN void mcpx_nl_init(const double* MCPX_NL_RESTRICT th, double* MCPX_NL_RESTRICT blk) {",
             "  (void)th;",
             "  (void)blk;",
@@ -481,6 +487,58 @@ class NLSystem:
             "}",
             "",
         ])
+
+    def _emit_band(self) -> list:
+        """The band kernel's part of the text (mcp_amd/band.py, csrc/ipm_nl_band.hpp): its tables,
+        mcpx_nl_init_c / mcpx_nl_eval_c — the generated code writing the compact array `cb`
+        (structural entries in block order, then G, then H) with the same CSE and expression
+        trees as mcpx_nl_init / mcpx_nl_eval, hence the same bits — and the lane-parallel
+        program on cb (MCPX_NL_CVEC).  MCPX_NL_CAN_BAND (whether the module gets the kernel)
+        and MCPX_NL_BAND_AUTO (whether MCPX_KERNEL_AUTO prefers it) are decided here, and
+        mcpx_nl_band_info carries them to the oracle's gcc build of the same text."""
+        from . import band as _band
+        from . import nl_vec
+
+        self.band = bp = _band.plan(self)
+        self.cvec = None
+        self.band_can = self.band_auto = False
+        if bp is None:
+            return ["#define MCPX_NL_CAN_BAND 0", "#define MCPX_NL_BAND_AUTO 0",
+                    "MCPX_NL_TABLE int32_t mcpx_nl_band_info[4] = {0, 0, 0, 0};",
+                    "MCPX_NL_TABLE int32_t mcpx_nl_band_rperm[1] = {0};",
+                    "MCPX_NL_TABLE int32_t mcpx_nl_band_cperm[1] = {0};"]
+        ci = lambda entries: [(bp.compact_index(self, i), e) for i, e in entries]
+        init = self._block(ci(self.const_entries), with_z=False, out="cb")
+        cse = {}
+        ev_entries = ci(self.var_entries + self.residuals)
+        ev = self._block(ev_entries, with_z=True, out="cb", cse_out=cse)
+        if cse:
+            self.cvec = nl_vec.build(self, cse["reps"], cse["red"], ev_entries, cse["names"], size=bp.csize)
+        ev_size = self.cvec.ev_size if self.cvec is not None else bp.csize + self.n + 2 * self.m
+        lds = bp.lds_bytes(ev_size)
+        self.band_lds = lds
+        can = BAND_KERNEL and lds <= BAND_LDS_LIMIT
+        auto = can and self.n > 64  # measured per size class: DESIGN.md §4 (band kernel)
+        self.band_can, self.band_auto = can, auto
+        return [
+            *bp.tables(),
+            f"#define MCPX_NL_CAN_BAND {int(can)}",
+            f"#define MCPX_NL_BAND_AUTO {int(auto)}",
+            f"MCPX_NL_TABLE int32_t mcpx_nl_band_info[4] = {{{int(can)}, {bp.ns}, {bp.wc}, {int(auto)}}};",
+            *(nl_vec.emit(self.cvec, "MCPX_NL_CVEC", "mcpx_nl_cvec") if self.cvec is not None else []),
+            "MCPX_NL_FN void mcpx_nl_init_c(const double* MCPX_NL_RESTRICT th, double* MCPX_NL_RESTRICT cb) {",
+            "  (void)th;",
+            "  (void)cb;",
+            *init,
+            "}",
+            "MCPX_NL_FN void mcpx_nl_eval_c(const double* MCPX_NL_RESTRICT th, const double* MCPX_NL_RESTRICT z,",
+            "                               double* MCPX_NL_RESTRICT cb) {",
+            "  (void)th;",
+            "  (void)z;",
+            "  (void)cb;",
+            *ev,
+            "}",
+        ]
 
     # ---- device module ---------------------------------------------------------
     def hip_source(self) -> str:

@@ -59,6 +59,7 @@ struct KernelArgs {
 hipError_t launch_ipm_spec(int family, int solver, int n, int m, const KernelArgs& a, int64_t batch,
                            hipStream_t st);
 hipError_t launch_ipm_schur_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
+hipError_t launch_ipm_schur_aff(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 hipError_t launch_ipm_red_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 hipError_t launch_ipm_red_aff(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);
 hipError_t launch_ipm_dense_qp(int nmax, const KernelArgs& a, int64_t batch, hipStream_t st);

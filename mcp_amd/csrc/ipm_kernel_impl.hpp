@@ -496,26 +496,29 @@ __device__ __forceinline__ double dot_strided(const double* __restrict__ p, int 
   return acc;
 }
 
-// SCHUR path (QP family), part 1: residuals.  x-lanes compute F_G, y-lanes
-// (which also own s_k) F_H and F_C; same fma order as family_row() of the
-// oracle.  `ta` is the A block with leading dimension `lda` (A_ki = ta[i·lda + k]),
-// followed at ta[n·lda] by b and ϕ: θ itself (lda = m) or the wave's LDS copy.
+// SCHUR path (QP family, and the affine family with ∂H/∂y ≡ 0), part 1: residuals.
+// x-lanes compute F_G, y-lanes (which also own s_k) F_H and F_C; same fma order as
+// family_row() of the oracle.  `ta` is the H-side coupling (QP: A; affine: R) with
+// leading dimension `lda` (A_ki = ta[i·lda + k]); `tq` / `ldq` the G-side coupling
+// negated in the same layout (QP: A again, since ∂G/∂y = −Aᵀ; affine: −Qᵀ); `tb` the
+// constants b then ϕ (affine: −h then −g, so that acc − b = acc + h bit for bit).
+// QP: θ itself (lda = m) or the wave's LDS copy, tq = ta, tb = ta + n·lda.
 template <int BATCH>
 __device__ __forceinline__ void qp_residuals(const double* __restrict__ th, const double* ta, int lda,
-                                             const double* zs, int ln, int n, int m, double eps, double s_own,
-                                             double& F, double& Fc) {
+                                             const double* tq, int ldq, const double* tb, const double* zs,
+                                             int ln, int n, int m, double eps, double s_own, double& F, double& Fc) {
   const bool rg = ln < n, rh = ln >= n && ln < n + m;
-  const int kh = ln - n, nl = n * lda;
+  const int kh = ln - n;
   const double* px = rg ? th + ln : (rh ? ta + kh : th);  // M column (θ) | A row
   const int sx = rg ? n : (rh ? lda : 0);
   double acc = dot_strided<BATCH, false>(px, sx, zs, n, 0.0);  // M_ij x_j  |  A_kj x_j
-  const double acc_y = dot_strided<BATCH, true>(ta + (rg ? ln * lda : 0), 1, zs + n, m, acc);  // − A_ki y_k
+  const double acc_y = dot_strided<BATCH, true>(tq + (rg ? ln * ldq : 0), 1, zs + n, m, acc);  // − A_ki y_k
   if (rg) acc = acc_y;
   F = 0.0;
   Fc = 0.0;
-  if (rg) F = acc - ta[nl + m + ln];                            // G = Mx − Aᵀy − ϕ
+  if (rg) F = acc - tb[m + ln];                                 // G = Mx − Aᵀy − ϕ
   if (rh) {
-    F = (acc - ta[nl + kh]) - s_own;                            // H − s
+    F = (acc - tb[kh]) - s_own;                                 // H − s
     Fc = s_own * zs[n + kh] - eps;                              // s⊙y − ϵ
   }
 }
@@ -661,11 +664,13 @@ __device__ __forceinline__ void fmac_row_bcast_self(double& acc, double nl) {
 #undef MCPX_FMAC_NB_SELF
 
 // Transposed Schur complement in the 2-D layout (see above).  acc[I][J][r].
-// `ta` / `lda`: the A block as in qp_residuals.
-template <int NT>
+// `ta` / `lda`: the A block as in qp_residuals.  TWO (affine family): the B fragment
+// comes from the negated G-side coupling tq / ldq (−Q_ik) instead of A_ki, so the
+// entries are S_ij = P_ij + Σ_k (−Q_ik)·(R_kj·D_k⁻¹) — the oracle's chain for either family.
+template <int NT, bool TWO = false>
 __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, const double* ta, int lda,
                                                  const double* sD, int ln, int n, int m, double tol,
-                                                 d4 (&acc)[NT][NT]) {
+                                                 d4 (&acc)[NT][NT], const double* tq = nullptr, int ldq = 0) {
   // lr ∈ [0, 3] made visible to the compiler (ln is opaque_lane in the Newton loop): with
   // compile-time (n, m) the range checks of the loads and masks below then fold away
   const int lr = (ln >> 4) & 3, lc = ln & 15;
@@ -693,27 +698,39 @@ __device__ __forceinline__ void qp_schur_form_2d(const double* __restrict__ th, 
         }
   }
   const int kc = (m + 3) / 4;
-  double nxt[NT];
+  double nxt[NT], nxq[TWO ? NT : 1];
 #pragma unroll
   for (int X = 0; X < NT; ++X) nxt[X] = ta[min(16 * X + lc, n - 1) * lda + min(lr, max(m - 1, 0))];
+  if constexpr (TWO) {
+#pragma unroll
+    for (int X = 0; X < NT; ++X) nxq[X] = tq[min(16 * X + lc, n - 1) * ldq + min(lr, max(m - 1, 0))];
+  }
   for (int c = 0; c < kc; ++c) {
     const int k = 4 * c + lr;
     const bool kin = k < m;
     const double dk = sD[kin ? k : 0];  // D_k⁻¹
-    double cur[NT];
+    double cur[NT], curq[TWO ? NT : 1];
 #pragma unroll
     for (int X = 0; X < NT; ++X) cur[X] = nxt[X];
+    if constexpr (TWO) {
+#pragma unroll
+      for (int X = 0; X < NT; ++X) curq[X] = nxq[X];
+    }
     if (c + 1 < kc) {
       const int k1 = min(k + 4, m - 1);
 #pragma unroll
       for (int X = 0; X < NT; ++X) nxt[X] = ta[min(16 * X + lc, n - 1) * lda + k1];
+      if constexpr (TWO) {
+#pragma unroll
+        for (int X = 0; X < NT; ++X) nxq[X] = tq[min(16 * X + lc, n - 1) * ldq + k1];
+      }
     }
     double af[NT], bf[NT];
 #pragma unroll
     for (int X = 0; X < NT; ++X) {
       const bool in = kin && 16 * X + lc < n;
-      af[X] = in ? cur[X] * dk : 0.0;  // A_kj · D_k⁻¹   (j = 16I + p)
-      bf[X] = in ? cur[X] : 0.0;       // A_ki         (i = 16J + q)
+      af[X] = in ? cur[X] * dk : 0.0;                    // A_kj · D_k⁻¹   (j = 16I + p)
+      bf[X] = in ? (TWO ? curq[X] : cur[X]) : 0.0;       // A_ki         (i = 16J + q)
     }
 #pragma unroll
     for (int I = 0; I < NT; ++I)
@@ -1095,16 +1112,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   // instance; they are read five times per Newton step (residual rows of G and of H,
   // rr, the Schur complement's MFMA fragments, δy), and from θ that traffic misses
   // L2 (PMC).  M stays in θ: with it the copy would cap occupancy.
-  constexpr bool LDSA = SCH && NC > 0 && MC > 0 && MCPX_LDS_A;
+  // Affine family under SCHUR (∂H/∂y ≡ 0, θ' = [P; Q; R; S; g; h], the S block not read):
+  // the same kernel with R in A's place and the G-side coupling −Qᵀ, with −h and −g, in
+  // the wave's LDS (sQ, odd stride) — Q is column-major in θ, so its rows are strided there.
+  constexpr bool AFF = SCH && FAMILY == MCPX_FAMILY_AFFINE;
+  constexpr bool LDSA = SCH && !AFF && NC > 0 && MC > 0 && MCPX_LDS_A;
   constexpr int LDA = LDSA ? MC + 1 : 1;
   __shared__ double sA[LDSA ? NC * LDA + MC + NC : 1];
   constexpr bool LDSM = LDSA && NC <= 16 && MCPX_LDS_M;  // M (column-major, as in θ) in LDS too
   __shared__ double sM[LDSM ? NC * NC : 1];
+  // n·(m + 1) + m + n doubles for n + m ≤ 64, n ≤ NMAX
+  constexpr int LQ = !AFF ? 1 : (NC > 0 ? NC * (MC + 1) + MC + NC : (NMAX >= 32 ? 1120 : NMAX * (65 - NMAX) + 64));
+  __shared__ double sQ[LQ];
   const int lane = threadIdx.x;
   const int64_t inst = blockIdx.x;
   const int n0 = NC ? NC : args.n, m0 = MC ? MC : args.m;
   const double* const th0 = args.theta + inst * args.theta_ld;
   const double tol = args.tol;
+  if constexpr (AFF) {  // −Qᵀ (row i at sQ[i·(m+1)]), then −h, −g
+    const int n = n0, m = m0, ldq = m + 1;
+    const double* tg = th0 + n * n;
+    for (int i = lane; i < n * m; i += 64) {
+      const int k = i / n, r = i - k * n;
+      sQ[r * ldq + k] = -tg[i];
+    }
+    const double* tc = th0 + n * n + 2 * n * m + m * m;  // g (n), h (m)
+    for (int i = lane; i < n + m; i += 64) sQ[n * ldq + (i < n ? m + i : i - n)] = -tc[i];
+    __syncthreads();
+  }
 
   // src/solver.jl:39-41, 64-66: x₀ = 0, y₀ = 1, s₀ = 1 unless warm-started.
   // DENSE: z = [x; y; s] one per lane.  RED: lanes [0,n) x, [n,n+m) (y, s).
@@ -1149,6 +1184,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
 #pragma unroll
       for (int b = 0; b < 8; ++b) asym |= (lane < n && j0 + b < n) && !(c[b] == t[b]);
     }
+    if constexpr (AFF) {  // and −Q = Rᵀ exactly (S symmetric for every D)
+      const int m = m0;
+      for (int i = lane; i < n * m; i += 64) {
+        const int r = i / m, k = i - r * m;
+        asym |= !(sQ[r * (m + 1) + k] == th0[n * n + n * m + i]);
+      }
+    }
     spd_try = ballot(asym) == 0ull;
     if constexpr (PASS == 1) {
       if (!spd_try) {  // needs the pivoting LU at every step: second pass
@@ -1177,8 +1219,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       const int NS = SCH ? n : (RED ? n + m : n + 2 * m);  // rows of the linear system
       const double* __restrict__ th = th0 + opaque64(0);  // stays a global pointer
       // SCHUR: the A block (then b, ϕ), from the wave's LDS copy when it has one
-      const double* const ta = LDSA ? (const double*)sA : th + n * n;
+      const double* const ta = LDSA ? (const double*)sA : th + (AFF ? n * n + n * m : n * n);
       const int lda = LDSA ? LDA : m;
+      // the negated G-side coupling and the constants (QP: A itself, then b, ϕ)
+      const int ldq = AFF ? m + 1 : lda;
+      const double* const tq = AFF ? (const double*)sQ : ta;
+      const double* const tb = AFF ? (const double*)sQ + n * ldq : ta + n * lda;
       const double* const tm = LDSM ? (const double*)sM : th;  // the M block
       const int ln = opaque_lane(lane);
       // ---- F!, ∇F_z! (:79-81) --------------------------------------------
@@ -1193,7 +1239,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       // quotient-per-use form costs (8 of them in the Schur K-loop).
       double rw = 1.0, Di = 1.0, ryr = 0.0;
       if constexpr (SCH) {
-        qp_residuals<MCPX_RES_BATCH>(tm, ta, lda, zs, ln, n, m, eps, s, F, Fc);
+        qp_residuals<MCPX_RES_BATCH>(tm, ta, lda, tq, ldq, tb, zs, ln, n, m, eps, s, F, Fc);
         rhs = -F;
         if (rh) {  // eliminate δs_k (pivot w_k) and then δy_k (pivot D_k)
           w = zs[ln] + tol;
@@ -1216,7 +1262,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
       if constexpr (SCH) {
         __syncthreads();
         // rr_i = −F_Gi + Σ_k A_ki ty_k  (x-lanes; other lanes' value unused)
-        rhs = dot_strided<8, false>(ta + (ln < n ? ln : 0) * lda, 1, sT, m, rhs);
+        rhs = dot_strided<8, false>(tq + (ln < n ? ln : 0) * ldq, 1, sT, m, rhs);
         sB[ln] = rhs;
       }
       MCPX_STAMP(1);
@@ -1230,7 +1276,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         constexpr int NT = (NMAX + 15) / 16;
         if (spd_try) {  // S formed transposed on the matrix cores, Gauss-Jordan in that layout
           d4 acc4[NT][NT];
-          qp_schur_form_2d<NT>(tm, ta, lda, sD, ln, n, m, tol, acc4);
+          qp_schur_form_2d<NT, AFF>(tm, ta, lda, sD, ln, n, m, tol, acc4, tq, ldq);
           MCPX_STAMP(2);
           double acc[NT][NT][4];
 #pragma unroll
@@ -1260,7 +1306,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
           // ds_bpermute: no n×n LDS tile, so LDS (2 KB per wave) does not cap occupancy
           constexpr int NT = (NMAX + 15) / 16;
           d4 acc4[NT][NT];
-          qp_schur_form_2d<NT>(tm, ta, lda, sD, ln, n, m, tol, acc4);
+          qp_schur_form_2d<NT, AFF>(tm, ta, lda, sD, ln, n, m, tol, acc4, tq, ldq);
           schur_rows_from_2d<NT, NMAX>(acc4, ln, n, a);
           rhs = sB[ln];
           ok = lu_solve_rows<NMAX>(a, rhs, (NC > 0) ? opaque(NS) : NS, ln, dz);

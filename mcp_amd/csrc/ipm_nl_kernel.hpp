@@ -996,6 +996,7 @@ __device__ __forceinline__ void solve(const KernelArgs& args) {
 #define MCPX_NL_CAN_WG_SCHUR (!MCPX_NL_HAS_S && MCPX_NL_N >= 1 && MCPX_NL_WG_LDS(MCPX_NL_N) <= MCPX_NL_WG_LIMIT)
 
 #include "sens_wg_impl.hpp"
+#include "ipm_nl_band.hpp"
 
 namespace mcpx {
 namespace nl {
@@ -1024,11 +1025,13 @@ constexpr int NVW = imax(1, N);
 }  // namespace mcpx
 
 // mcpx_nl_meta: {layout version, n, m, p, has_s, kernel mask, block size, nnz, nnz of ∇F_θ,
-// 0, 0, 0}; kernel mask: bit MCPX_LINSOLVE_* = one-wave kernel, bit 3 + MCPX_LINSOLVE_* =
+// the band kernel's workspace doubles per slot, 0, 0}; kernel mask: bit MCPX_LINSOLVE_* = one-wave kernel, bit 3 + MCPX_LINSOLVE_* =
 // workgroup kernel, bit MCPX_MODULE_VJP / MCPX_MODULE_JVP = sensitivity kernels (the
 // VJP factors the (n+m)-dim system of the REDUCED workgroup solver, the JVP the full
 // (n+2m)-dim ∇F_z of the DENSE one: they exist when those fit LDS), bit MCPX_MODULE_SCHUR_MW =
-// the 4-wave SCHUR kernel mcpx_nl_solve_schur_mw (layout 4)
+// the 4-wave SCHUR kernel mcpx_nl_solve_schur_mw (layout 4); bits MCPX_MODULE_BAND /
+// MCPX_MODULE_BAND_AUTO = the band SCHUR kernel mcpx_nl_solve_band (ipm_nl_band.hpp) and whether
+// MCPX_KERNEL_AUTO prefers it (both decided by codegen.py: MCPX_NL_CAN_BAND, MCPX_NL_BAND_AUTO)
 extern "C" {
 __device__ int32_t mcpx_nl_meta[12] = {
     4, MCPX_NL_N, MCPX_NL_M, MCPX_NL_P, MCPX_NL_HAS_S,
@@ -1036,9 +1039,18 @@ __device__ int32_t mcpx_nl_meta[12] = {
         (MCPX_NL_CAN_SCHUR << MCPX_LINSOLVE_SCHUR) | (MCPX_NL_CAN_WG_REDUCED << (3 + MCPX_LINSOLVE_REDUCED)) |
         (MCPX_NL_CAN_WG_DENSE << (3 + MCPX_LINSOLVE_DENSE)) | (MCPX_NL_CAN_WG_SCHUR << (3 + MCPX_LINSOLVE_SCHUR)) |
         (MCPX_NL_CAN_WG_REDUCED << MCPX_MODULE_VJP) | (MCPX_NL_CAN_WG_DENSE << MCPX_MODULE_JVP) |
-        (MCPX_NL_CAN_SCHUR_MW << MCPX_MODULE_SCHUR_MW),
-    MCPX_NL_SIZE, MCPX_NL_NNZ, MCPX_NL_NNZ_T, 0, 0, 0};
+        (MCPX_NL_CAN_SCHUR_MW << MCPX_MODULE_SCHUR_MW) | (MCPX_NL_CAN_BAND << MCPX_MODULE_BAND) |
+        ((MCPX_NL_CAN_BAND && MCPX_NL_BAND_AUTO) << MCPX_MODULE_BAND_AUTO),
+    MCPX_NL_SIZE, MCPX_NL_NNZ, MCPX_NL_NNZ_T,
+#if MCPX_NL_CAN_BAND
+    (int32_t)mcpx::nl::band::WS,
+#else
+    0,
+#endif
+    0, 0};
 
+// MCPX_NL_ONLY_BAND (experiments, never set by codegen.py): compile the band kernel alone
+#ifndef MCPX_NL_ONLY_BAND
 #if MCPX_NL_CAN_WG_REDUCED
 __global__ __launch_bounds__(mcpx::wg::kThreads) void mcpx_nl_vjp_wg(const mcpx::wg::WgSensArgs args) {
   mcpx::wg::sens_instances<MCPX_FAMILY_NONLINEAR, false, mcpx::nl::NVW, MCPX_NL_N + MCPX_NL_M, mcpx::nl::Gen>(args);
@@ -1068,6 +1080,11 @@ __global__ __launch_bounds__(mcpx::wg::kThreads) void mcpx_nl_solve_schur_wg(con
 }
 #endif
 
+#endif  // MCPX_NL_ONLY_BAND
+#if MCPX_NL_CAN_BAND
+__global__ __launch_bounds__(64) void mcpx_nl_solve_band(const mcpx::wg::WgArgs args) { mcpx::nl::band::solve(args); }
+#endif
+#ifndef MCPX_NL_ONLY_BAND
 #if MCPX_NL_CAN_REDUCED
 __global__ __launch_bounds__(64) void mcpx_nl_solve_reduced(const mcpx::KernelArgs args) {
   mcpx::nl::solve<MCPX_LINSOLVE_REDUCED>(args);
@@ -1088,4 +1105,5 @@ __global__ __launch_bounds__(256) void mcpx_nl_solve_schur_mw(const mcpx::Kernel
   mcpx::nl::solve<MCPX_LINSOLVE_SCHUR, true>(args);
 }
 #endif
+#endif  // MCPX_NL_ONLY_BAND
 }  // extern "C"

@@ -101,11 +101,13 @@ int pick_wg_bucket(int N) {
 // *wg: the solve runs on the workgroup-per-instance kernels (ipm_wg_impl.hpp);
 // *nmax: the one-wave kernels' row width, or the workgroup kernels' dimension bucket.
 int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* nmax,
-            const mcpx_module* mod = nullptr, bool* wg = nullptr, bool* mw = nullptr) {
-  bool wg_local = false, mw_local = false;
+            const mcpx_module* mod = nullptr, bool* wg = nullptr, bool* mw = nullptr, bool* band = nullptr) {
+  bool wg_local = false, mw_local = false, band_local = false;
   if (!wg) wg = &wg_local;
   if (!mw) mw = &mw_local;
+  if (!band) band = &band_local;
   *mw = false;
+  *band = false;
   if (!d || !p) return fail(MCPX_EINVAL, "desc and params must be non-NULL");
   int64_t pd;
   if (mod) {  // a generated nonlinear module: θ dimension and sizes from its metadata
@@ -129,7 +131,7 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   if (ls != MCPX_LINSOLVE_REDUCED && ls != MCPX_LINSOLVE_DENSE && ls != MCPX_LINSOLVE_SCHUR)
     return fail(MCPX_EINVAL, "unknown linear_solver %d", ls);
   if (p->kernel != MCPX_KERNEL_AUTO && p->kernel != MCPX_KERNEL_WAVE && p->kernel != MCPX_KERNEL_WORKGROUP &&
-      p->kernel != MCPX_KERNEL_MULTIWAVE)
+      p->kernel != MCPX_KERNEL_MULTIWAVE && p->kernel != MCPX_KERNEL_BAND)
     return fail(MCPX_EINVAL, "unknown kernel selector %d", p->kernel);
   bool wave_ok, wg_ok;
   if (mod) {
@@ -139,12 +141,20 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
     if (p->kernel == MCPX_KERNEL_MULTIWAVE && !mw_ok)
       return fail(MCPX_EUNSUPPORTED, "the generated module has no multi-wave kernel for linear_solver=%d", ls);
     *mw = mw_ok && p->kernel == MCPX_KERNEL_MULTIWAVE;  // measured slower than one wave: opt-in
+    // the band kernel (ipm_nl_band.hpp): forced, or AUTO when the module prefers it or has no
+    // one-wave SCHUR kernel (oracle/ipm_oracle.c picks lu_band_solve by the same rule)
+    const bool band_ok = ls == MCPX_LINSOLVE_SCHUR && ((mod->meta[5] >> MCPX_MODULE_BAND) & 1);
+    const bool band_auto = band_ok && ((mod->meta[5] >> MCPX_MODULE_BAND_AUTO) & 1);
+    if (p->kernel == MCPX_KERNEL_BAND && !band_ok)
+      return fail(MCPX_EUNSUPPORTED, "the generated module has no band kernel for linear_solver=%d", ls);
+    *band = p->kernel == MCPX_KERNEL_BAND || (p->kernel == MCPX_KERNEL_AUTO && band_ok && (band_auto || !wave_ok));
     *nmax = 0;
   } else {
     if (p->kernel == MCPX_KERNEL_MULTIWAVE)
       return fail(MCPX_EUNSUPPORTED, "MCPX_KERNEL_MULTIWAVE is a generated module's SCHUR kernel");
-    if (ls == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP)
-      return fail(MCPX_EINVAL, "linear_solver=schur needs the QP family (dH/dy = 0)");
+    if (p->kernel == MCPX_KERNEL_BAND)
+      return fail(MCPX_EUNSUPPORTED, "MCPX_KERNEL_BAND is a generated module's SCHUR kernel");
+    // (affine family: ∂H/∂y is taken as 0 — the S block of θ' is not read, include/mcpx.h)
     const int N = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : (ls == MCPX_LINSOLVE_REDUCED ? d->n + d->m : d->n);
     const int lanes = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : d->n + d->m;  // one wave: one lane per row
     wave_ok = pick_nmax(N) > 0 && lanes <= MCPX_MAX_KKT_DIM;
@@ -153,7 +163,7 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
   }
   if (p->kernel == MCPX_KERNEL_WAVE) wg_ok = false;
   if (p->kernel == MCPX_KERNEL_WORKGROUP) wave_ok = false;
-  if (*mw) wave_ok = true;
+  if (*mw || *band) wave_ok = true;
   if (!wave_ok && !wg_ok) {
     if (mod)
       return fail(MCPX_EUNSUPPORTED, "the generated module has no %s kernel for linear_solver=%d (n=%d m=%d)",
@@ -243,7 +253,7 @@ hipError_t launch(int nmax, const mcpx::KernelArgs& a, int64_t nb, hipStream_t s
     case MCPX_LINSOLVE_DENSE:
       return qp ? mcpx::launch_ipm_dense_qp(nmax, a, nb, st) : mcpx::launch_ipm_dense_aff(nmax, a, nb, st);
     default:
-      return mcpx::launch_ipm_schur_qp(nmax, a, nb, st);
+      return qp ? mcpx::launch_ipm_schur_qp(nmax, a, nb, st) : mcpx::launch_ipm_schur_aff(nmax, a, nb, st);
   }
 }
 
@@ -334,9 +344,54 @@ int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const d
   return rc;
 }
 
+// The band SCHUR kernel of a generated module (ipm_nl_band.hpp): one wave per resident slot
+// on the work queue of the workgroup kernels, no workspace (LDS and VGPRs only).
+int launch_band(const mcpx_desc* d, const double* theta, const double* x0, const double* y0, const double* s0,
+                const mcpx_out* o, mcpx::KernelArgs a, hipStream_t st, mcpx_module* mod) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  hipModule_t hm;
+  int rc = module_on(mod, dev, &hm);
+  if (rc) return rc;
+  hipFunction_t f = nullptr;
+  if (hipModuleGetFunction(&f, hm, "mcpx_nl_solve_band") != hipSuccess)
+    return fail(MCPX_EUNSUPPORTED, "the generated module has no band kernel");
+  int per_cu = 0, cus = 0;
+  HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 64, 0));
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t slots_max = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+  // the kernel's per-slot HBM workspace (its U rows when they exceed its VGPR budget, mcpx_nl_meta[9])
+  const int64_t stride = ((int64_t)mod->meta[9] + 31) / 32 * 32;
+  const int64_t grid_max = std::min(slots_max, std::min((int64_t)1 << 30, d->batch));
+  double* ws = nullptr;
+  HIP_TRY(pool_malloc((void**)&ws, sizeof(double) * (size_t)(grid_max * stride) + 256, st));
+  int32_t* counter = (int32_t*)(ws + grid_max * stride);
+  mcpx::wg::WgArgs w{};
+  w.counter = counter;
+  w.work = ws;
+  w.slot_stride = stride;
+  const int64_t CH = (int64_t)1 << 30;
+  for (int64_t b0 = 0; b0 < d->batch && rc == MCPX_OK; b0 += CH) {
+    const int64_t nb = std::min(CH, d->batch - b0);
+    const int grid = (int)std::min(grid_max, nb);
+    set_chunk(a, d, theta, x0, y0, s0, o, b0);
+    w.k = a;
+    w.batch = nb;
+    hipError_t e = hipMemsetAsync(counter, 0, sizeof(int32_t), st);
+    if (e == hipSuccess) {
+      void* params[] = {&w};
+      e = hipModuleLaunchKernel(f, (unsigned)grid, 1, 1, 64, 1, 1, 0, st, params, nullptr);
+    }
+    if (e != hipSuccess) rc = fail(MCPX_EHIP, "band solver launch failed: %s", hipGetErrorString(e));
+  }
+  HIP_TRY(hipFreeAsync(ws, st));
+  return rc;
+}
+
 int launch_chunks(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                   const double* s0, const mcpx_out* o, mcpx::KernelArgs a, int nmax, hipStream_t st,
-                  mcpx_module* mod = nullptr, bool wg = false, bool mw = false) {
+                  mcpx_module* mod = nullptr, bool wg = false, bool mw = false, bool band = false) {
+  if (band) return launch_band(d, theta, x0, y0, s0, o, a, st, mod);
   if (wg) return launch_wg(d, theta, x0, y0, s0, o, a, nmax, st, mod);
   hipFunction_t nlf = nullptr;  // generated module: its kernel, launched by hipModuleLaunchKernel
   if (mod) {
@@ -514,8 +569,8 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   if (rc) return rc;
   mcpx::KernelArgs a;
   int nmax;
-  bool wg = false, mw = false;
-  if ((rc = prepare(d, prm, &a, &nmax, mod, &wg, &mw))) return rc;
+  bool wg = false, mw = false, band = false;
+  if ((rc = prepare(d, prm, &a, &nmax, mod, &wg, &mw, &band))) return rc;
   const int n = d->n, m = d->m;
   const int64_t W = mask_words(m);
   PipeLease lease;
@@ -579,7 +634,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
     od.fail_reason = fr.p ? fr.p + c0 : nullptr;
     mcpx_desc dd = *d;
     dd.batch = cn;
-    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, cs, mod, wg, mw))) return rc;
+    if ((rc = launch_chunks(&dd, th[k].p, wx[k].p, wy[k].p, ws[k].p, &od, a, nmax, cs, mod, wg, mw, band))) return rc;
     HIP_TRY(hipEventRecord(P->consumed[k], cs));
   }
   HIP_TRY(hipStreamSynchronize(us));
@@ -932,15 +987,15 @@ int solve_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta,
                       void* stream) {
   mcpx::KernelArgs a;
   int nmax;
-  bool wg = false, mw = false;
-  int rc = prepare(d, prm, &a, &nmax, mod, &wg, &mw);
+  bool wg = false, mw = false, band = false;
+  int rc = prepare(d, prm, &a, &nmax, mod, &wg, &mw, &band);
   if (rc) return rc;
   if (!outputs_ok(o)) return fail(MCPX_EINVAL, "required output arrays missing");
   if (d->batch == 0) return MCPX_OK;
   if (!theta) return fail(MCPX_EINVAL, "theta is NULL");
   int dev = 0;
   if ((rc = current_device(&dev))) return rc;
-  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod, wg, mw);
+  return launch_chunks(d, theta, x0, y0, s0, o, a, nmax, (hipStream_t)stream, mod, wg, mw, band);
 }
 
 // mcpx_solve_vjp_batch_device: the solve kernels with the pullback in their epilogue

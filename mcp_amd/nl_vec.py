@@ -243,11 +243,12 @@ class Program:
         return blk
 
 
-def build(nl, reps, red, entries, names) -> Program | None:
+def build(nl, reps, red, entries, names, size: int | None = None) -> Program | None:
     """The chain program of the eval block (entries = [(blk index, expr)], reps/red = the CSE
-    the C text was printed from, names = the printer's Symbol → operand map of z / θ).
-    None when an expression is not polynomial or the ev array would not fit 16-bit byte
-    offsets."""
+    the C text was printed from, names = the printer's Symbol → operand map of z / θ; `size` =
+    doubles of the block array the entries index, nl.size by default — the band kernel's
+    compact array is smaller).  None when an expression is not polynomial or the ev array
+    would not fit 16-bit byte offsets."""
     atom_of = {}
     for sym, txt in names.items():
         if txt.startswith("th["):
@@ -267,7 +268,7 @@ def build(nl, reps, red, entries, names) -> Program | None:
             b.chains.append(terms)
     except Unsupported:
         return None
-    prog = Program(nl.n, nl.m, nl.p, nl.size, b.chains, outputs)
+    prog = Program(nl.n, nl.m, nl.p, nl.size if size is None else size, b.chains, outputs)
     if prog.ev_size * 8 >= 65536:
         return None
     steps, _, _ = prog.tables()
@@ -281,26 +282,27 @@ def build(nl, reps, red, entries, names) -> Program | None:
 MAX_WORDS, MAX_SLOTS = 64, 32  # VGPR budget of eval_vec's word and destination tables
 
 
-def emit(prog: Program) -> list:
+def emit(prog: Program, macro: str = "MCPX_NL_VEC", name: str = "mcpx_nl_vec") -> list:
     """C lines of the tables (generated module text): the ev layout, the constants, the term
     steps per slot (a macro list, for compile-time unrolling), per (slot, step) the 64 lanes'
-    operand words and per slot the 64 destinations."""
+    operand words and per slot the 64 destinations.  (`macro` / `name`: MCPX_NL_CVEC /
+    mcpx_nl_cvec for the band kernel's program on the compact array.)"""
     steps, words, dsts = prog.tables()
     lit = lambda v: ("-" if np.signbit(v) else "") + float(abs(v)).hex()
     flat = lambda rows: ", ".join(str(x) for r in rows for x in r)
     return [
         "/* lane-parallel eval (mcp_amd/nl_vec.py): chains of one rounding per product and sum, the",
         "   outputs and CSE temporaries of mcpx_nl_eval in the same operation order, 64 chains per slot */",
-        "#define MCPX_NL_VEC 1",
-        f"#define MCPX_NL_VEC_EV {prog.ev_size}",
-        f"#define MCPX_NL_VEC_OFF_Z {prog.off_z}",
-        f"#define MCPX_NL_VEC_OFF_T {prog.off_t}",
-        f"#define MCPX_NL_VEC_OFF_C {prog.off_c}",
-        f"#define MCPX_NL_VEC_NC {len(prog.consts)}",
-        f"#define MCPX_NL_VEC_NSLOT {len(steps)}",
-        f"#define MCPX_NL_VEC_NWORD {len(words)}",
-        f"#define MCPX_NL_VEC_STEPS {', '.join(map(str, steps))}",
-        f"MCPX_NL_TABLE double mcpx_nl_vec_const[{len(prog.consts)}] = {{{', '.join(lit(v) for v in prog.consts)}}};",
-        f"MCPX_NL_TABLE uint32_t mcpx_nl_vec_word[{len(words) * 64}] = {{{flat(words)}}};",
-        f"MCPX_NL_TABLE uint32_t mcpx_nl_vec_dst[{len(dsts) * 64}] = {{{flat(dsts)}}};",
+        f"#define {macro} 1",
+        f"#define {macro}_EV {prog.ev_size}",
+        f"#define {macro}_OFF_Z {prog.off_z}",
+        f"#define {macro}_OFF_T {prog.off_t}",
+        f"#define {macro}_OFF_C {prog.off_c}",
+        f"#define {macro}_NC {len(prog.consts)}",
+        f"#define {macro}_NSLOT {len(steps)}",
+        f"#define {macro}_NWORD {len(words)}",
+        f"#define {macro}_STEPS {', '.join(map(str, steps))}",
+        f"MCPX_NL_TABLE double {name}_const[{len(prog.consts)}] = {{{', '.join(lit(v) for v in prog.consts)}}};",
+        f"MCPX_NL_TABLE uint32_t {name}_word[{len(words) * 64}] = {{{flat(words)}}};",
+        f"MCPX_NL_TABLE uint32_t {name}_dst[{len(dsts) * 64}] = {{{flat(dsts)}}};",
     ]

@@ -54,6 +54,22 @@ def unpack_parameters(theta: np.ndarray, num_primals: int, num_inequalities: int
     return dict(M=M, A=A, b=b, phi=phi)
 
 
+def affine_embedding(theta: np.ndarray, num_primals: int, num_inequalities: int) -> np.ndarray:
+    """The QP θ = [vec M; vec A; b; ϕ] as affine-family data θ' = [vec P; vec Q; vec R; vec S; g; h]
+    (include/mcpx.h): P = M, Q = −Aᵀ, R = A, S = 0, g = −ϕ, h = −b — what the Julia shim's
+    `affine_parameters` hands over for the benchmark's PrimalDualMCP."""
+    n, m = num_primals, num_inequalities
+    th = np.atleast_2d(np.asarray(theta, dtype=np.float64))
+    B = th.shape[0]
+    M = th[:, :n * n]
+    A = th[:, n * n:n * n + m * n].reshape(B, n, m)  # [b, i, k] = A_ki (column-major m×n)
+    b = th[:, n * n + m * n:n * n + m * n + m]
+    phi = th[:, n * n + m * n + m:n * n + m * n + m + n]
+    Q = -A.transpose(0, 2, 1)  # [b, k, i] = Q_ik (column-major n×m)
+    return np.ascontiguousarray(np.concatenate([M, Q.reshape(B, -1), A.reshape(B, -1), np.zeros((B, m * m)),
+                                                -phi, -b], 1))
+
+
 def generate_random_parameter_torch(generator, num_primals: int, num_inequalities: int,
                                     batch: int, sparsity_rate: float = 0.0, device="cuda"):
     """Same distribution and layout, generated directly in device memory with torch

@@ -84,7 +84,9 @@ class OracleNL(C.Structure):
     _fields_ = [("init", C.c_void_p), ("eval", C.c_void_p), ("p", C.c_int32), ("has_s", C.c_int32),
                 ("size", C.c_int32), ("wave_schur", C.c_int32), ("qk_ptr", C.c_void_p), ("qk_idx", C.c_void_p),
                 ("rj_ptr", C.c_void_p), ("rj_idx", C.c_void_p), ("eval_theta", C.c_void_p),
-                ("tc_ptr", C.c_void_p), ("tc_idx", C.c_void_p), ("tr_ptr", C.c_void_p), ("tr_idx", C.c_void_p)]
+                ("tc_ptr", C.c_void_p), ("tc_idx", C.c_void_p), ("tr_ptr", C.c_void_p), ("tr_idx", C.c_void_p),
+                ("band", C.c_int32), ("band_ns", C.c_int32), ("band_wc", C.c_int32), ("band_auto", C.c_int32),
+                ("band_rperm", C.c_void_p), ("band_cperm", C.c_void_p)]
 
 
 _GEN_DIR = os.path.join(_HERE, "_build", "gen")
@@ -114,7 +116,9 @@ def nl_lib(nl):
                     "  switch (which) { case 0: return mcpx_nl_qk_ptr; case 1: return mcpx_nl_qk_idx;\n"
                     "    case 2: return mcpx_nl_rj_ptr; case 3: return mcpx_nl_rj_idx;\n"
                     "    case 4: return mcpx_nl_tc_ptr; case 5: return mcpx_nl_tc_idx;\n"
-                    "    case 6: return mcpx_nl_tr_ptr; default: return mcpx_nl_tr_idx; }\n}\n")
+                    "    case 6: return mcpx_nl_tr_ptr; case 7: return mcpx_nl_tr_idx;\n"
+                    "    case 8: return mcpx_nl_band_info; case 9: return mcpx_nl_band_rperm;\n"
+                    "    default: return mcpx_nl_band_cperm; }\n}\n")
         tmp = f"{so}.{os.getpid()}.tmp"
         subprocess.run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
                         "-o", tmp, src, "-lm"], check=True)
@@ -129,10 +133,11 @@ def _nl_spec(nl) -> OracleNL:
     G.oracle_nl_table.restype = C.c_void_p
     G.oracle_nl_table.argtypes = [C.c_int]
     fn = lambda f: C.cast(f, C.c_void_p).value
-    t = [G.oracle_nl_table(w) for w in range(8)]
+    t = [G.oracle_nl_table(w) for w in range(11)]
+    info = (C.c_int32 * 4).from_address(t[8])  # mcpx_nl_band_info of the same generated text
     return OracleNL(fn(G.oracle_nl_init), fn(G.oracle_nl_eval), nl.p, int(nl.has_s), nl.size,
                     int(nl.solvers()["schur"]), *t[:4],
-                    fn(G.oracle_nl_eval_theta), *t[4:])
+                    fn(G.oracle_nl_eval_theta), *t[4:8], info[0], info[1], info[2], info[3], t[9], t[10])
 
 
 def solve_batch_nl(nl, theta: np.ndarray, *, x0=None, y0=None, s0=None, params: Params | None = None,

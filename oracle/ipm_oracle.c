@@ -102,6 +102,12 @@ typedef struct oracle_nl {
    * for a solve). */
   void (*eval_theta)(const double* th, const double* z, double* dth);
   const int32_t *tc_ptr, *tc_idx, *tr_ptr, *tr_idx;
+  /* the band kernel (mcp_amd/band.py, csrc/ipm_nl_band.hpp; mcpx_nl_band_info of the generated
+   * text): band = the module has it, band_auto = MCPX_KERNEL_AUTO prefers it; S' = S[σ][:, π]
+   * with σ = band_rperm, π = band_cperm (S' row / column → original index), window rows
+   * ≤ k + band_ns − 1, window columns [k, k + band_wc − 1] */
+  int32_t band, band_ns, band_wc, band_auto;
+  const int32_t *band_rperm, *band_cperm;
 } oracle_nl;
 
 /* doubles of the block array, the S block always included (zero when absent) */
@@ -142,6 +148,10 @@ int oracle_build_tables(const mcpx_params* p, oracle_tables* t) {
 
 /* ---- problem families: residual row + Jacobian row (src/mcp.jl:72-120) ---- */
 
+/* The affine family under linear_solver = SCHUR: ∂H/∂y is taken as 0, the S block of θ'
+ * is not read (include/mcpx.h) — family_row skips it; oracle-internal code. */
+#define FAMILY_AFFINE_NOS 100
+
 /* Row i of F and of ∇F (without tol·I) at z = [x; y; s]. */
 static double family_row(int family, int n, int m, const double* th, const double* z,
                          double eps, int i, double* row) {
@@ -173,7 +183,7 @@ static double family_row(int family, int n, int m, const double* th, const doubl
       for (int j = 0; j < n; ++j) row[j] = P[(size_t)j * n + i];
       for (int k = 0; k < m; ++k) row[n + k] = Q[(size_t)k * n + i];
       return th[(size_t)n * n + 2 * (size_t)n * m + i];
-    } else { /* G = P x + Q y + g */
+    } else { /* G = P x + Q y + g (FAMILY_AFFINE_NOS too) */
       const double* P = th;
       const double* Q = th + (size_t)n * n;
       const double* g = th + (size_t)n * n + 2 * (size_t)n * m + (size_t)m * m;
@@ -214,10 +224,11 @@ static double family_row(int family, int n, int m, const double* th, const doubl
         row[j] = R[(size_t)j * m + k];
         acc = fma(row[j], x[j], acc);
       }
-      for (int q = 0; q < m; ++q) {
-        row[n + q] = S[(size_t)q * m + k];
-        acc = fma(row[n + q], y[q], acc);
-      }
+      if (family == MCPX_FAMILY_AFFINE) /* FAMILY_AFFINE_NOS: S not read (SCHUR, ∂H/∂y ≡ 0) */
+        for (int q = 0; q < m; ++q) {
+          row[n + q] = S[(size_t)q * m + k];
+          acc = fma(row[n + q], y[q], acc);
+        }
       return (acc + h[k]) - s[k];
     }
   } else { /* s ⊙ y − ϵ rows */
@@ -316,6 +327,69 @@ static int gj_spd_solve(int n, double* S /* n×n row-major, destroyed */, double
   return 0;
 }
 
+/* Band LU with partial pivoting of S' = S[σ][:, π] (the generated modules' band kernel,
+ * csrc/ipm_nl_band.hpp; mcp_amd/band.py orders the columns for a narrow elimination window, as
+ * UMFPACK's symbolic phase orders the columns of its sparse LU, src/solver.jl:50,61,83, and the
+ * rows by their first nonzero column).  Rows enter the window in S' row order: rows 0 .. ns − 1
+ * before step 0, row k + ns after step k; every row with a nonzero in column k is in the window
+ * at step k, and every window row lies inside the columns [k, k + wc − 1].  Step k searches the
+ * remaining window rows with lu_solve_x's first-max rule (largest |a_ik|, ties to the lowest S'
+ * row, NaN never wins, all-NaN → the first remaining window row; an exact zero pivot is the
+ * failed solve) and updates every other remaining window row in the columns k + 1 .. k + wc − 1
+ * and the rhs with lu_solve_x's rcp = 1 arithmetic (l_i = a_ik · (1 / piv),
+ * a_ij ← fma(−l_i, u_j, a_ij)); the back substitution takes x_k = b_p · (1 / u_pk) and updates
+ * the pivot rows of steps k − wc + 1 .. k − 1.  On finite values the skipped terms are exact
+ * zeros, so this is the dense LU with partial pivoting of S' (a row permutation only changes
+ * which of equal |a_ik| wins).  S, rr: original order; dz: the solution in original order.
+ * Returns 0 ok, 1 on a zero pivot. */
+static int lu_band_solve(int n, const double* S, const double* rr, double* dz, const int32_t* rperm,
+                         const int32_t* cperm, int ns, int wc, double* Sp, double* b, double* x, int* rem,
+                         int* prow) {
+  for (int r = 0; r < n; ++r) {
+    for (int c = 0; c < n; ++c) Sp[(size_t)r * n + c] = S[(size_t)rperm[r] * n + cperm[c]];
+    b[r] = rr[rperm[r]];
+    rem[r] = 1;
+  }
+  for (int k = 0; k < n; ++k) {
+    const int hi = k + ns - 1 < n - 1 ? k + ns - 1 : n - 1;
+    int best = -1;
+    double bv = -1.0;
+    for (int i = 0; i <= hi; ++i) {
+      if (!rem[i]) continue;
+      const double v = fabs(Sp[(size_t)i * n + k]);
+      if (v > bv) { bv = v; best = i; }
+    }
+    if (best < 0)
+      for (int i = 0; i <= hi; ++i)
+        if (rem[i]) { best = i; break; }
+    const double piv = Sp[(size_t)best * n + k];
+    if (piv == 0.0) return 1;
+    rem[best] = 0;
+    prow[k] = best;
+    const double rp = 1.0 / piv;
+    const int jhi = k + wc - 1 < n - 1 ? k + wc - 1 : n - 1;
+    const double* u = Sp + (size_t)best * n;
+    for (int i = 0; i <= hi; ++i) {
+      if (!rem[i]) continue;
+      double* a = Sp + (size_t)i * n;
+      const double l = a[k] * rp;
+      for (int j = k + 1; j <= jhi; ++j) a[j] = fma(-l, u[j], a[j]);
+      b[i] = fma(-l, b[best], b[i]);
+    }
+  }
+  for (int k = n - 1; k >= 0; --k) {
+    const int p = prow[k];
+    const double xk = b[p] * (1.0 / Sp[(size_t)p * n + k]);
+    x[k] = xk;
+    for (int t = (k - wc + 1 > 0 ? k - wc + 1 : 0); t < k; ++t) {
+      const int q = prow[t];
+      b[q] = fma(-Sp[(size_t)q * n + k], xk, b[q]);
+    }
+  }
+  for (int k = 0; k < n; ++k) dz[cperm[k]] = x[k];
+  return 0;
+}
+
 static int lu_solve(int N, double* J, double* b, double* dz, int* remaining, int* step_of, int* prow) {
   return lu_solve_x(N, J, b, dz, remaining, step_of, prow, 0);
 }
@@ -391,11 +465,21 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
     nl->init(th, w->blk);
     fth = w->blk;
   }
-  if (p->linear_solver == MCPX_LINSOLVE_SCHUR && d->family == MCPX_FAMILY_QP) {
+  const int schur_dense = p->linear_solver == MCPX_LINSOLVE_SCHUR && !nl;
+  const int fam = (schur_dense && d->family == MCPX_FAMILY_AFFINE) ? FAMILY_AFFINE_NOS : d->family;
+  if (schur_dense) {
     m_sym = 1;
     for (int i = 0; i < n && m_sym; ++i)
       for (int j = 0; j < n; ++j)
         if (!(th[(size_t)j * n + i] == th[(size_t)i * n + j])) { m_sym = 0; break; }
+    /* affine: and −Q = Rᵀ exactly (then S = P − Q·D⁻¹·R is symmetric for every D) */
+    if (d->family == MCPX_FAMILY_AFFINE)
+      for (int i = 0; i < n && m_sym; ++i)
+        for (int k = 0; k < m; ++k)
+          if (!(-th[(size_t)n * n + (size_t)k * n + i] == th[(size_t)n * n + (size_t)n * m + (size_t)i * m + k])) {
+            m_sym = 0;
+            break;
+          }
   }
   while (kkt > p->tol && eps > p->tol && outer < p->max_outer_iters) { /* :71 */
     int inner = 1;            /* :72 */
@@ -404,7 +488,7 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
       /* :79-82 F!, ∇F_z!, A = ∇F + tol I, b = −F */
       if (nl) nl->eval(th, z, w->blk);
       for (int i = 0; i < N; ++i) {
-        w->F[i] = family_row(d->family, n, m, fth, z, eps, i, w->J + (size_t)i * N);
+        w->F[i] = family_row(fam, n, m, fth, z, eps, i, w->J + (size_t)i * N);
         w->J[(size_t)i * N + i] += p->tol;
         w->b[i] = -w->F[i];
       }
@@ -416,8 +500,9 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           break;
         }
       } else if (p->linear_solver == MCPX_LINSOLVE_SCHUR) {
-        /* slack block, then the diagonal y block: n×n Schur complement (QP family) */
-        const int m4 = d->family == MCPX_FAMILY_QP ? (m + 3) / 4 * 4 : m; /* QP: the MFMA's K padding */
+        /* slack block, then the diagonal y block: n×n Schur complement (QP / affine family:
+           S_ij = P_ij + Σ_k (−Q_ik)·(R_kj·D_k⁻¹), the QP's A_ki·(A_kj·D_k⁻¹)) */
+        const int m4 = !nl ? (m + 3) / 4 * 4 : m; /* QP / affine: the MFMA's K padding */
         for (int k = 0; k < m; ++k) {
           const int h = n + k, c = n + m + k;
           const double rwk = 1.0 / w->J[(size_t)c * N + c];  /* 1 / (y_k + tol) */
@@ -482,9 +567,21 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
           memcpy(w->bs, w->b, sizeof(double) * n);
           spd_ok = gj_spd_solve(n, w->Js, w->bs, w->dz) == 0;
         }
-        /* generated modules: Gauss-Jordan on the one-wave kernels, LU on the workgroup ones */
+        /* generated modules, as the C ABI picks the kernel (mcpx_api.cpp prepare): the band kernel
+           (MCPX_KERNEL_BAND, or AUTO when the module prefers it or has no one-wave SCHUR kernel),
+           the one-wave Gauss-Jordan (rcp = 2), else the workgroup kernels' LU (rcp = 1) */
+        const int band = nl && nl->band &&
+                         (p->kernel == MCPX_KERNEL_BAND ||
+                          (p->kernel == MCPX_KERNEL_AUTO && (nl->band_auto || !nl->wave_schur)));
         const int xmode = !nl ? 0 : ((nl->wave_schur && p->kernel != MCPX_KERNEL_WORKGROUP) ? 2 : 1);
-        if (!spd_ok && lu_solve_x(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow, xmode)) {
+        if (band) {
+          if (lu_band_solve(n, w->Jr, w->b, w->dz, nl->band_rperm, nl->band_cperm, nl->band_ns, nl->band_wc, w->Js,
+                            w->bs, w->row, w->remaining, w->prow)) {
+            status = MCPX_STATUS_FAILED;
+            reason |= MCPX_FAIL_LINSOLVE;
+            break;
+          }
+        } else if (!spd_ok && lu_solve_x(n, w->Jr, w->b, w->dz, w->remaining, w->step_of, w->prow, xmode)) {
           status = MCPX_STATUS_FAILED;
           reason |= MCPX_FAIL_LINSOLVE;
           break;
@@ -662,7 +759,8 @@ int oracle_solve_batch(const mcpx_desc* d, const double* theta, const double* x0
   if (!d || !theta || !p || !outputs_ok(o)) return MCPX_EINVAL;
   const int64_t pd = oracle_theta_dim(d->family, d->n, d->m);
   if (pd < 0 || d->n + d->m < 1 || d->batch < 0 || d->theta_ld < pd) return MCPX_EINVAL;
-  if (p->linear_solver == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP) return MCPX_EINVAL;
+  if (p->linear_solver == MCPX_LINSOLVE_SCHUR && d->family != MCPX_FAMILY_QP && d->family != MCPX_FAMILY_AFFINE)
+    return MCPX_EINVAL;
   return run_batch(d, theta, x0, y0, s0, p, o, nthreads, NULL);
 }
 

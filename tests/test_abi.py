@@ -105,9 +105,13 @@ def test_size_limits():
     assert _call(desc, np.zeros(_abi.theta_dim(0, 400, 200)), _abi.make_params()) == _abi.MCPX_EUNSUPPORTED
 
 
-def test_schur_needs_qp_family():
+def test_schur_takes_the_affine_family_on_one_wave():
+    """SCHUR accepts the affine family (∂H/∂y taken as 0, include/mcpx.h); it is one wave only."""
     desc = _abi.Desc(1, 2, 2, 0, 1, _abi.theta_dim(1, 2, 2))
-    assert _call(desc, np.zeros(64), _abi.make_params(linear_solver="schur")) == _abi.MCPX_EINVAL
+    assert _call(desc, np.zeros(64), _abi.make_params(linear_solver="schur")) in (_abi.MCPX_OK, _abi.MCPX_ENODEV)
+    desc = _abi.Desc(1, 40, 30, 0, 1, _abi.theta_dim(1, 40, 30))
+    assert _call(desc, np.zeros(_abi.theta_dim(1, 40, 30)),
+                 _abi.make_params(linear_solver="schur")) == _abi.MCPX_EUNSUPPORTED
 
 
 def test_no_device_is_an_error_not_a_fallback():

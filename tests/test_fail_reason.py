@@ -47,8 +47,6 @@ CASES = list(cases())
 @pytest.mark.parametrize("ls", ["reduced", "dense", "schur"])
 def test_oracle_fail_reason(oracle_lib, case, ls):
     label, fam, n, m, th, kw, bit = case
-    if ls == "schur" and fam != _abi.FAMILY_QP:
-        pytest.skip("SCHUR is the QP family's")
     r = oracle_lib.solve_batch(fam, n, m, th, linear_solver=ls, **kw)
     fr, st, outer = r["fail_reason"], r["status"], r["outer_iters"]
     maxo = kw.get("max_outer_iters", 50)
@@ -72,8 +70,6 @@ def test_gpu_fail_reason_vs_oracle(gpu, oracle_lib, case, ls):
     from tests.test_gpu_parity import assert_parity
 
     label, fam, n, m, th, kw, _ = case
-    if ls == "schur" and fam != _abi.FAMILY_QP:
-        pytest.skip("SCHUR is the QP family's")
     got = solve_batch(fam, n, m, th, linear_solver=ls, trace_len=64, **kw)
     ref = oracle_lib.solve_batch(fam, n, m, th, linear_solver=ls, trace_len=64, **kw)
     assert_parity(got, ref)

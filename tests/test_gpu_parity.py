@@ -206,9 +206,9 @@ def test_unsupported_sizes(gpu, oracle_lib):
     with pytest.raises(MCPXError):
         solve_batch(0, 400, 200, th, linear_solver="dense")  # n + 2m = 800 > 768
     from mcp_amd import _abi as abi
-    tha = np.zeros((1, abi.theta_dim(1, 4, 4)))
+    tha = np.zeros((1, abi.theta_dim(1, 40, 30)))
     with pytest.raises(MCPXError):
-        solve_batch(1, 4, 4, tha, linear_solver="schur")  # schur needs the QP family
+        solve_batch(1, 40, 30, tha, linear_solver="schur")  # affine SCHUR is one wave: n + m ≤ 64
 
 
 def test_device_api_matches_host_api(gpu):

@@ -102,8 +102,8 @@ def test_oracle_param_validation(oracle_lib):
         with pytest.raises(ValueError):
             oracle_lib.solve_batch(0, 3, 2, th, **bad)
     tha = np.zeros((1, 4 * 4 + 2 * 4 * 4 + 4 * 4 + 8))
-    with pytest.raises(ValueError):  # schur needs the QP family
-        oracle_lib.solve_batch(1, 4, 4, tha, linear_solver="schur")
+    r = oracle_lib.solve_batch(1, 4, 4, tha, linear_solver="schur")  # affine SCHUR: ∂H/∂y taken as 0
+    assert r["status"].shape == (1,)
 
 
 def test_oracle_threads_deterministic(oracle_lib):

@@ -148,3 +148,44 @@ def test_lane_change_generated_jacobian_matches_finite_differences(oracle_lib):
         np.testing.assert_allclose(Q, J[:n, n:], atol=1e-7 * scale)
         np.testing.assert_allclose(R, J[n:, :n], atol=1e-7 * scale)
         assert not nl.has_s and np.abs(J[n:, n:]).max() <= 1e-7 * scale  # ∂H/∂y ≡ 0 (SCHUR applies)
+
+
+def _c4_batch(T, B):
+    from mcp_amd.lane_change import LaneChangeGame
+    from mcp_amd.qp_benchmark import chunked_slice
+
+    game = LaneChangeGame(T)
+    th = chunked_slice(lambda rng, k: game.generate_random_parameter(rng, k), 1, 0, B)  # bench.py --lane-change
+    return game.mcp.nl, np.ascontiguousarray(game.mcp.theta_map(th))
+
+
+@pytest.mark.slow
+def test_c4_oracle_modes_equal_full_lu_on_solved_games(oracle_lib):
+    """BASELINE C4 (the bench's 1,024 lane-change games at T = 2, tol 1e-6): the SCHUR step as
+    the one-wave kernel runs it (Gauss-Jordan with partial pivoting, lu_solve_x rcp = 2) and as
+    the workgroup kernels run it (LU + substitution, rcp = 1) against the literal dense LU of
+    the full (n + 2m) = 140-dim ∇F + tol·I (src/solver.jl:81-83).  On the 974 games all three
+    solve, every discrete output (status, outer and Newton counts, α traces, active sets) is
+    identical and the iterates agree to ≤ 1e-10.  The 50 games that fail after 931 Newton steps
+    fail under every mode; rounding moves some of their trajectories, and those divergences are
+    recorded here exactly (as on the QP sparse stress set above)."""
+    nl, th = _c4_batch(2, 1024)
+    run = lambda **kw: oracle_lib.solve_batch_nl(nl, th, tol=1e-6, nthreads=8, trace_len=TRACE, **kw)
+    r = {"wave": run(linear_solver="schur"), "wg": run(linear_solver="schur", kernel="workgroup"),
+         "dense": run(linear_solver="dense")}
+    d = r["dense"]
+    ok = d["status"] == 0
+    assert int(ok.sum()) == 974
+    expect = {"wave": (16, 17, 32), "wg": (16, 18, 31)}  # failing games: Newton counts, active sets, α traces
+    for mode, a in ((k, r[k]) for k in ("wave", "wg")):
+        assert np.array_equal(a["status"], d["status"]), mode
+        assert np.array_equal(a["outer_iters"], d["outer_iters"]), mode
+        diff = {k: (a[k] != d[k]).reshape(len(ok), -1).any(1)
+                for k in ("newton_iters", "active_mask", "alpha_trace")}
+        for k, v in diff.items():
+            assert not v[ok].any(), (mode, k)
+        assert tuple(int(v.sum()) for v in diff.values()) == expect[mode], mode
+        rel = np.abs(_z(a)[ok] - _z(d)[ok]).max(1) / np.maximum(1.0, np.abs(_z(d)[ok]).max(1))
+        assert rel.max() <= 1e-10, (mode, rel.max())
+        for k in ("kkt_error", "eps"):
+            assert np.all(np.abs(a[k][ok] - d[k][ok]) <= 1e-8 * np.maximum(1.0, np.abs(d[k][ok]))), (mode, k)

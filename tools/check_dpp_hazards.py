@@ -170,9 +170,12 @@ def wait_state_hazards(insts, want: str):
             if ll:
                 # a join point: another predecessor (a branch to this label) may have
                 # written the source just before jumping; only the fall-through path
-                # is walked, so a reader this close to a label is reported unless it
-                # is padded on its own
-                bad.append(f"WAIT-STATE HAZARD (join point {tt}) in {k}:\n   {t}  ({states} wait states after the label)")
+                # is walked, so an asm reader this close to a label is reported unless
+                # it is padded on its own.  A compiler-emitted DPP (a builtin, outside
+                # asm) is padded by the compiler's hazard recognizer, which follows
+                # every predecessor block.
+                if asm:
+                    bad.append(f"WAIT-STATE HAZARD (join point {tt}) in {k}:\n   {t}  ({states} wait states after the label)")
                 break
             o = tt.split()[0]
             if o == "s_nop":

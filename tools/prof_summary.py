@@ -1,6 +1,6 @@
 """Summarise a tools/gpu_profile.sh run into profiles/<round>/.
 
-    python tools/prof_summary.py gpurun_out/prof_c3 [--dst profiles/r04] [--kernel ipm_solve_kernel]
+    python tools/prof_summary.py gpurun_out/prof_c3 [--dst profiles/r05] [--kernel ipm_solve_kernel]
 
 The source folder holds bench.json (the bench line of the profiled command),
 cmd.txt (that command), trace/ (rocprofv3 --kernel-trace --stats of the same
@@ -50,7 +50,7 @@ def timed_window(cmd: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
-    ap.add_argument("--dst", default=os.path.join(ROOT, "profiles", "r04"))
+    ap.add_argument("--dst", default=os.path.join(ROOT, "profiles", "r05"))
     ap.add_argument("--kernel", default="")
     a = ap.parse_args()
     bench = json.loads(open(os.path.join(a.src, "bench.json")).read().strip().splitlines()[-1])
