@@ -505,7 +505,7 @@ def main_lane_change(a, world, rank, local, dist, pl):
                 f"seeded SeedSequence({a.seed}, spawn_key=(chunk,))), uploaded to HBM before timing",
         "config": {"workload": f"BASELINE C4: 2-player lane-change game T={a.lane_change} "
                                f"(n={n}, m={m}, KKT dim {N}), fp64, global batch {pl['global_batch']}, tol={a.tol:g}",
-                   "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "batch_per_gpu": B,
+                   "n": n, "m": m, "kkt_dim": N, "linear_solver": ls, "batch_per_gpu": B, "kernel": kernel,
                    "global_batch": pl["global_batch"], "parallelism": f"dp{world} (instance shards)"},
         "roofline": rl,
         "newton_iters_mean": newton_all / pl["global_batch"], "success_rate": solved_all / pl["global_batch"],
@@ -525,7 +525,7 @@ def main_lane_change(a, world, rank, local, dist, pl):
         cb = cpu_baseline(lambda k, t: coracle.solve_batch_nl(mcp.nl, theta_host[:k], tol=a.tol, linear_solver=ls,
                                                               kernel=a.kernel, nthreads=t),
                           B, a, th, "C oracle with the generated host G/H code (same algorithm and linear solver)",
-                          per_thread=256 if a.lane_change <= 2 else 4)
+                          per_thread=256 if a.lane_change <= 2 else 32)
         r = cb.pop("_result")
         k = len(r["status"])
         got = {f: out[f][:k].cpu().numpy() for f in C4_FIELDS}

@@ -905,19 +905,57 @@ __device__ __forceinline__ bool gj2d_spd(double (&acc)[NT][NT][4], double (&rh)[
 // pass, which takes the exact rcp_uniform of gj2d_spd — so the bits stay the oracle's.  Per
 // pivot the bookkeeping is 2 readlanes, the 7-instruction reciprocal, one product per half, the
 // pivot-row zeroing by a constant lane mask (2 v_cndmask, no compare) and the pivot recorded in
-// its lane by 2 v_writelane for the final division.  (Recording it instead by a one-lane
-// ds_write under an EXEC switch, no VALU, gave wrong last bits on the GPU in every instance:
-// tools/parity_probe.py, profiles/r04; not kept.)
+// its lane by 2 v_writelane for the final division.
+//
+// MCPX_GJ_PIVREC = 1 (diagnostic, off): the round-4 variant that records each pivot by a
+// one-lane ds_write under an EXEC switch instead (record_pivot).  It gave wrong last bits in
+// every instance.  Cause: pivot 0's ds_write reads the accumulator register the Schur MFMA has
+// just written, 2-6 instructions later, where a 16x16x4 f64 MFMA result needs 19 before an LDS
+// store reads it as data — hipcc pads that for its own instructions, not inside asm, and the
+// store took the register's stale value (tools/check_dpp_hazards.py rule 4).
+// MCPX_GJ_PIVREC_PAD = 1 adds that distance (s_nop) ahead of pivot 0's store; the EXEC write →
+// store s_nop 4 of round 4 is always there.
 #ifndef MCPX_GJ_LOOKAHEAD
 #define MCPX_GJ_LOOKAHEAD 1
 #endif
 #ifndef MCPX_GJ_ZMASK
 #define MCPX_GJ_ZMASK 1
 #endif
+#ifndef MCPX_GJ_PIVREC
+#define MCPX_GJ_PIVREC 0
+#endif
+#ifndef MCPX_GJ_PIVREC_PAD
+#define MCPX_GJ_PIVREC_PAD 0
+#endif
+#ifndef MCPX_GJ_PIVREC_SETPAD  // s_nop 4 between the EXEC write and the store
+#define MCPX_GJ_PIVREC_SETPAD 1
+#endif
+#ifndef MCPX_GJ_PIVREC_EXECPAD  // s_nop 4 after the EXEC restore (ahead of the next DPP fmac)
+#define MCPX_GJ_PIVREC_EXECPAD 1
+#endif
+#define MCPX_PR_STR2(x) #x
+#define MCPX_PR_STR(x) MCPX_PR_STR2(x)
+#define MCPX_PR_SET MCPX_PR_STR(MCPX_GJ_PIVREC_SETPAD)
+#define MCPX_PR_EXEC MCPX_PR_STR(MCPX_GJ_PIVREC_EXECPAD)
+typedef __attribute__((address_space(3))) double lds_f64;
 // The pivot of step K, the entry `v` holds in lane LANE, to LDS slot K of `base` by a one-lane
-// ds_write under a constant EXEC mask (no VALU; the Gauss-Jordan's final division reads it).
-// (The lane mask passes through an opaque asm first: as a plain "s" constant the compiler
-// hoists all 16 distinct masks out of the Newton loop and spills SGPRs.)
+// ds_write under a constant EXEC mask.  (The lane mask passes through an opaque asm first: as a
+// plain "s" constant the compiler hoists all the distinct masks out of the Newton loop.)
+template <int K, int LANE, bool PAD>
+__device__ __forceinline__ void record_pivot(uint32_t base, double v) {
+  uint64_t save, msk = 1ull << LANE;
+  asm volatile("" : "+s"(msk));
+  // (".rept 0" emits nothing: the pads are switched by the macros above)
+  if (PAD)
+    asm volatile("s_nop 7\n s_nop 7\n s_nop 3\n s_mov_b64 %0, exec\n s_mov_b64 exec, %3\n"
+                 " .rept " MCPX_PR_SET "\n s_nop 4\n .endr\n"
+                 " ds_write_b64 %1, %2 offset:%4\n s_mov_b64 exec, %0\n .rept " MCPX_PR_EXEC "\n s_nop 4\n .endr"
+                 : "=&s"(save) : "v"(base), "v"(v), "s"(msk), "n"(8 * K) : "memory");
+  else
+    asm volatile("s_mov_b64 %0, exec\n s_mov_b64 exec, %3\n .rept " MCPX_PR_SET "\n s_nop 4\n .endr\n"
+                 " ds_write_b64 %1, %2 offset:%4\n s_mov_b64 exec, %0\n .rept " MCPX_PR_EXEC "\n s_nop 4\n .endr"
+                 : "=&s"(save) : "v"(base), "v"(v), "s"(msk), "n"(8 * K) : "memory");
+}
 // v with the lanes lc = R of every DPP row replaced by +0: two v_cndmask_b32, no compare.
 template <int R>
 __device__ __forceinline__ double zero_lanes(double v) {
@@ -930,7 +968,7 @@ __device__ __forceinline__ double zero_lanes(double v) {
 
 template <int NT, int NN, int K>
 __device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&rh)[NT], int ln, double& piv,
-                                             double& rp, double (&col)[NT], double& dgl) {
+                                             double& rp, double (&col)[NT], double& dgl, uint32_t pbase) {
   constexpr int Jk = K >> 4, Rk = K & 15;
   constexpr bool NX = K + 1 < NN;
   constexpr int K1 = NX ? K + 1 : K;
@@ -966,7 +1004,8 @@ __device__ __forceinline__ void gj2d_la_step(double (&acc)[NT][NT][4], double (&
 #pragma unroll
     for (int J = 0; J < NT; ++J) col[J] = bperm_f64_addr(acc[In][J][rn], (16 * Qn + lc) << 2);
     piv = bcast(acc[In][Jn][rn], 16 * Qn + Rn);
-    dgl = writelane_f64(dgl, piv, K1);  // pivot K + 1 in lane K + 1 (the final division)
+    if constexpr (MCPX_GJ_PIVREC) record_pivot<K1, 16 * Qn + Rn, false>(pbase, acc[In][Jn][rn]);
+    else dgl = writelane_f64(dgl, piv, K1);  // pivot K + 1 in lane K + 1 (the final division)
     rp = rcp_fast(piv);
   }
 #pragma unroll
@@ -1013,14 +1052,23 @@ __device__ __forceinline__ bool gj2d_spd_la(std::integer_sequence<int, K...>, do
                                             double (&rh)[NT], int ln, double& xo) {
   const int lc = ln & 15;
   double col[NT];
+  __shared__ double spiv[MCPX_GJ_PIVREC ? NN : 1];  // MCPX_GJ_PIVREC: pivot k in slot k
+  const uint32_t pbase = (uint32_t)(uintptr_t)(lds_f64*)spiv;
   double piv = bcast(acc[0][0][0], 0);  // pivot 0: column 0 = tile 0, element 0, DPP row 0
-  double dgl = writelane_f64(1.0, piv, 0);  // pivot k in lane k
+  double dgl = 1.0;
+  if constexpr (MCPX_GJ_PIVREC) record_pivot<0, 0, MCPX_GJ_PIVREC_PAD>(pbase, acc[0][0][0]);
+  else dgl = writelane_f64(1.0, piv, 0);  // pivot k in lane k
   double rp = rcp_fast(piv);
 #pragma unroll
   for (int J = 0; J < NT; ++J) col[J] = bperm_f64_addr(acc[0][J][0], lc << 2);
-  (gj2d_la_step<NT, NN, K>(acc, rh, ln, piv, rp, col, dgl), ...);
+  (gj2d_la_step<NT, NN, K>(acc, rh, ln, piv, rp, col, dgl, pbase), ...);
   // every pivot > 0 and inside the fast reciprocal's exact range, checked once at the end
   // (a bad pivot only made the later steps compute discarded values); lane i holds pivot i
+  if constexpr (MCPX_GJ_PIVREC) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the asm ds_writes
+    __builtin_amdgcn_wave_barrier();
+    dgl = spiv[ln < NN ? ln : 0];
+  }
   const double d = dgl;
   if (ballot((ln < NN) & !((d > 0.0) & rcp_fast_ok(d)))) return false;
   double r = rh[0];

@@ -342,13 +342,19 @@ __device__ __forceinline__ void eval_cvec(double* ev, const uint32_t (&w)[MCPX_N
 }
 #endif
 
+// MCPX_BAND_DEBUG_EXIT (diagnostic builds only, tools/band_debug.py): 1 return at entry, 2 leave
+// the work loop at its first instance, 3 no Jacobian init and no Newton loop, 4 no Newton loop.
+#ifndef MCPX_BAND_DEBUG_EXIT
+#define MCPX_BAND_DEBUG_EXIT 0
+#endif
+
 // The Newton loop of one instance after another (work queue), src/solver.jl:35-121.
 __device__ __forceinline__ void solve(const wg::WgArgs& A) {
+  if (MCPX_BAND_DEBUG_EXIT == 1) return;
   const KernelArgs& args = A.k;
   __shared__ __attribute__((aligned(16))) double ev[EVN];
   __shared__ double Sc[NNZ + 1], rrp[n], sDi[imax(1, m)], sTy[imax(1, m)], dxp[n], img2[2 * WC];
   __shared__ double Ush[ULDS ? n * US : 1];
-  __shared__ int s_inst;
   double* const cb = ev;
   double* const zs = ev + OFFZ;
   const int ln0 = threadIdx.x;
@@ -367,11 +373,14 @@ __device__ __forceinline__ void solve(const wg::WgArgs& A) {
   for (int r = 0; r < RNB; ++r) ipx[r] = ln0 + 64 * r < n ? mcpx_nl_band_iperm[ln0 + 64 * r] : 0;
   for (;;) {
     const int ln = ln0;
-    if (ln == 0) s_inst = atomicAdd(A.counter, 1);
-    __syncthreads();
-    const int64_t inst = __builtin_amdgcn_readfirstlane(s_inst);
-    __syncthreads();
-    if (inst >= A.batch) break;
+    // the next instance, taken in uniform control flow: every lane adds (lane 0 one, the others
+    // zero) and lane 0's old value is the wave's.  (A one-lane `if (ln == 0)` atomic through LDS, as
+    // the workgroup kernels do, let the compiler — its barrier being a no-op for a one-wave
+    // workgroup — thread the loop's end-of-instance `if (ln == 0)` stores straight into that
+    // atomic, so the other 63 lanes re-read the old instance forever: a hang.)
+    const int got = atomicAdd(A.counter, ln == 0 ? 1 : 0);
+    const int64_t inst = __builtin_amdgcn_readfirstlane(got);
+    if (inst >= A.batch || MCPX_BAND_DEBUG_EXIT == 2) break;
     const double* __restrict__ th = args.theta + inst * args.theta_ld;
     // src/solver.jl:39-41, 64-66
 #pragma unroll
@@ -391,11 +400,11 @@ __device__ __forceinline__ void solve(const wg::WgArgs& A) {
     for (int k = ln; k < MCPX_NL_P; k += 64) ev[MCPX_NL_CVEC_OFF_T + k] = th[k];
 #endif
     __syncthreads();
-    if (ln == 0) mcpx_nl_init_c(th, cb);
+    if (ln == 0 && MCPX_BAND_DEBUG_EXIT != 3) mcpx_nl_init_c(th, cb);
     double eps = 1.0, kkt = __builtin_huge_val();  // :67-68
     int status = 0, outer = 1, newton = 0;         // :69-70
     unsigned reason = 0;
-    while (kkt > tol && eps > tol && outer < args.max_outer) {  // :71
+    while (kkt > tol && eps > tol && outer < args.max_outer && MCPX_BAND_DEBUG_EXIT < 3) {  // :71
       int inner = 1;
       status = 0;
       while (kkt > eps && inner < args.max_inner) {  // :75

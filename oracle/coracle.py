@@ -279,3 +279,34 @@ def jvp_batch_nl(nl, theta, x, y, s, theta_dot, nthreads: int = 1):
     if rc != 0:
         raise ValueError(f"oracle_jvp_batch_nl failed with code {rc}")
     return zd, st
+
+
+def cond_batch(family: int, n: int, m: int, theta, x, y, s, nthreads: int = 1, nl=None):
+    """Oracle of mcpx_cond_batch[_module]: the Hager–Higham reciprocal 1-norm condition estimate
+    of ∇F_z at (x, y, s) (oracle/ipm_oracle.c cond_estimate) → (rcond (B,), status (B,))."""
+    theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+    B, ld = theta.shape
+    if nl is not None:
+        n, m = nl.n, nl.m
+    x, y, s = _f64(x, (B, n)), _f64(y, (B, m)), _f64(s, (B, m))
+    rc_ = np.empty(B)
+    st = np.empty(B, np.int32)
+    L = lib()
+    if not hasattr(L, "_cond_ready"):
+        L.oracle_cond_batch.restype = C.c_int
+        L.oracle_cond_batch.argtypes = [C.POINTER(Desc)] + [C.c_void_p] * 6 + [C.c_int]
+        L.oracle_cond_batch_nl.restype = C.c_int
+        L.oracle_cond_batch_nl.argtypes = [C.POINTER(Desc)] + [C.c_void_p] * 6 + [C.c_int, C.POINTER(OracleNL)]
+        L._cond_ready = True
+    args = (_ptr(theta), _ptr(x), _ptr(y), _ptr(s), _ptr(rc_), _ptr(st), int(nthreads))
+    if nl is not None:
+        from mcp_amd._abi import FAMILY_NONLINEAR
+
+        desc = Desc(FAMILY_NONLINEAR, n, m, 0, B, ld)
+        rc = L.oracle_cond_batch_nl(C.byref(desc), *args, C.byref(_nl_spec(nl)))
+    else:
+        desc = Desc(family, n, m, 0, B, ld)
+        rc = L.oracle_cond_batch(C.byref(desc), *args)
+    if rc != 0:
+        raise ValueError(f"oracle_cond_batch failed with code {rc}")
+    return rc_, st

@@ -65,6 +65,7 @@
  * Build with -ffp-contract=off (oracle/Makefile) so that only the explicit
  * fma() calls fuse.
  */
+#include <float.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -827,7 +828,7 @@ typedef struct sens_ws {
 static int sens_ws_alloc(sens_ws* w, int N) {
   const size_t NN = (size_t)(N > 0 ? N : 1);
   w->J = (double*)malloc(sizeof(double) * NN * NN);
-  w->JT = (double*)malloc(sizeof(double) * NN * NN);
+  w->JT = (double*)malloc(sizeof(double) * (NN * NN > 4 * NN ? NN * NN : 4 * NN)); /* also cond_estimate's 4 vectors */
   w->b = (double*)malloc(sizeof(double) * NN);
   w->dz = (double*)malloc(sizeof(double) * NN);
   w->z = (double*)malloc(sizeof(double) * NN);
@@ -865,8 +866,138 @@ static void jacobian_z(int family, int n, int m, const double* th, const double*
   for (int i = 0; i < N; ++i) (void)family_row(family, n, m, th, z, 0.0, i, J + (size_t)i * N);
 }
 
+/* ---- condition estimate of ∇F_z (the matrix of the rrule's solve, src/AutoDiff.jl:39) ----
+ * The reference solves qr(−∇F_z, ColumnNorm()) \ ∇F_θ; at degenerate solutions ∇F_z is nearly
+ * singular and QR and LU answers can differ at O(1).  rcond = 1 / (‖∇F_z‖₁ · est‖∇F_z⁻¹‖₁), the
+ * Hager–Higham 1-norm estimate (Higham, "FORTRAN codes for estimating the one-norm of a real or
+ * complex matrix", ACM TOMS 14 (1988), Algorithm 4.1 with its alternative lower bound) from one
+ * LU with partial pivoting — the kernels' (csrc/sens_wg_impl.hpp cond_instances) op for op:
+ *   factor   lu_solve's elimination (division multipliers, first-max pivots) with l_ik kept in
+ *            A[i][k]; an exact zero pivot: rcond = 0, status 1;
+ *   A x = b  forward: for k ascending, rows pivoted later take b_i = fma(−l_ik, b_{p_k}, b_i);
+ *            back: x_k = b_{p_k} / u_{p_k k}, rows pivoted earlier b_i = fma(−u_ik, x_k, b_i);
+ *   Aᵀz = c  (PA = LU) Uᵀ: u_k = c_k / u_{p_k k}, columns i > k take c_i = fma(−u_{p_k i}, u_k, c_i);
+ *            Lᵀ: for k descending, v_k = u_k, j < k take u_j = fma(−l_{p_k j}, v_k, u_j); z_{p_k} = v_k;
+ *   Hager    x = 1/N; at most 5 rounds: y = A⁻¹x, γ = Σ|y_k| (ascending); stop if round > 0 and
+ *            not γ > γ_prev; ξ = sign(y) (+1 for y ≥ 0); stop if round > 0 and ξ is unchanged;
+ *            z = A⁻ᵀξ; j = first argmax |z_i| (NaN never wins, none: 0); stop if round > 0 and
+ *            not |z_j| > z_{j_prev}; x = e_j;
+ *   alt      b_i = (−1)ⁱ (1 + i/(N−1)), γ = max(γ, 2·Σ|A⁻¹b| / (3N));
+ *   rcond    ‖A‖₁ = max over columns of the column sums of |a_ij| (rows ascending); rcond =
+ *            1 / (‖A‖₁ · γ), 0 when that product is 0 or not finite. */
+static int lu_factor_keep(int N, double* J, int* remaining, int* step_of, int* prow) {
+  for (int i = 0; i < N; ++i) remaining[i] = 1;
+  for (int k = 0; k < N; ++k) {
+    int best = -1;
+    double bv = -1.0;
+    for (int i = 0; i < N; ++i) {
+      if (!remaining[i]) continue;
+      const double v = fabs(J[(size_t)i * N + k]);
+      if (v > bv) { bv = v; best = i; }
+    }
+    if (best < 0)
+      for (int i = 0; i < N; ++i)
+        if (remaining[i]) { best = i; break; }
+    const double piv = J[(size_t)best * N + k];
+    if (piv == 0.0) return 1;
+    remaining[best] = 0;
+    step_of[best] = k;
+    prow[k] = best;
+    const double* u = J + (size_t)best * N;
+    for (int i = 0; i < N; ++i) {
+      if (!remaining[i]) continue;
+      double* a = J + (size_t)i * N;
+      const double l = a[k] / piv;
+      for (int j = k + 1; j < N; ++j) a[j] = fma(-l, u[j], a[j]);
+      a[k] = l;
+    }
+  }
+  return 0;
+}
+
+static void lu_apply(int N, const double* J, const int* step_of, const int* prow, double* b, double* x) {
+  for (int k = 0; k < N; ++k) {
+    const double bp = b[prow[k]];
+    for (int i = 0; i < N; ++i)
+      if (step_of[i] > k) b[i] = fma(-J[(size_t)i * N + k], bp, b[i]);
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    const int p = prow[k];
+    const double xk = b[p] / J[(size_t)p * N + k];
+    x[k] = xk;
+    for (int i = 0; i < N; ++i)
+      if (step_of[i] < k) b[i] = fma(-J[(size_t)i * N + k], xk, b[i]);
+  }
+}
+
+static void lu_apply_t(int N, const double* J, const int* prow, double* c, double* z) {
+  for (int k = 0; k < N; ++k) {
+    const double* u = J + (size_t)prow[k] * N;
+    const double uk = c[k] / u[k];
+    c[k] = uk;
+    for (int i = k + 1; i < N; ++i) c[i] = fma(-u[i], uk, c[i]);
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    const double* l = J + (size_t)prow[k] * N;
+    const double vk = c[k];
+    for (int j = 0; j < k; ++j) c[j] = fma(-l[j], vk, c[j]);
+    z[prow[k]] = vk;
+  }
+}
+
+/* J: N×N row-major ∇F_z (destroyed); v: 4·N doubles of scratch.  Returns rcond, *singular. */
+static double cond_estimate(int N, double* J, int* remaining, int* step_of, int* prow, double* v, int* singular) {
+  double anorm = 0.0;
+  for (int j = 0; j < N; ++j) {
+    double c = 0.0;
+    for (int i = 0; i < N; ++i) c = c + fabs(J[(size_t)i * N + j]);
+    if (c > anorm || c != c) anorm = c;
+    if (anorm != anorm) break;
+  }
+  *singular = lu_factor_keep(N, J, remaining, step_of, prow);
+  if (*singular) return 0.0;
+  double *x = v, *y = v + N, *xi = v + 2 * N, *z = v + 3 * N;
+  const double inv = 1.0 / (double)N;
+  for (int i = 0; i < N; ++i) x[i] = inv;
+  double est = 0.0;
+  int jprev = -1;
+  for (int it = 0; it < 5; ++it) {
+    lu_apply(N, J, step_of, prow, x, y); /* x destroyed */
+    double g = 0.0;
+    for (int k = 0; k < N; ++k) g = g + fabs(y[k]);
+    if (it > 0 && !(g > est)) break;
+    est = g;
+    int same = it > 0;
+    for (int k = 0; k < N; ++k) {
+      const double sg = y[k] >= 0.0 ? 1.0 : -1.0;
+      if (sg != xi[k]) same = 0;
+      xi[k] = sg;
+    }
+    if (same) break;
+    for (int k = 0; k < N; ++k) x[k] = xi[k]; /* x: the rhs of the transposed solve */
+    lu_apply_t(N, J, prow, x, z);
+    int jm = -1;
+    double bz = -1.0;
+    for (int i = 0; i < N; ++i)
+      if (fabs(z[i]) > bz) { bz = fabs(z[i]); jm = i; }
+    if (jm < 0) jm = 0;
+    if (it > 0 && !(fabs(z[jm]) > z[jprev])) break;
+    for (int i = 0; i < N; ++i) x[i] = 0.0;
+    x[jm] = 1.0;
+    jprev = jm;
+  }
+  for (int i = 0; i < N; ++i) x[i] = (i & 1 ? -1.0 : 1.0) * (1.0 + (N > 1 ? (double)i / (double)(N - 1) : 0.0));
+  lu_apply(N, J, step_of, prow, x, y);
+  double g = 0.0;
+  for (int k = 0; k < N; ++k) g = g + fabs(y[k]);
+  const double alt = 2.0 * g / (3.0 * (double)N);
+  if (alt > est) est = alt;
+  const double den = anorm * est;
+  return (den > 0.0 && den <= DBL_MAX) ? 1.0 / den : 0.0;
+}
+
 typedef struct sens_job {
-  int jvp;
+  int jvp; /* 0 VJP, 1 JVP, 2 condition estimate (out[b] = rcond) */
   const mcpx_desc* d;
   const double *theta, *x, *y, *s, *gx, *gy, *gs, *tdot;
   int K;
@@ -1034,6 +1165,11 @@ static void sens_one(const sens_job* j, sens_ws* w, int64_t b) {
       for (int i = 0; i < n; ++i) o[nn + 2 * nm + mm + i] = -lx[i];                        /* ∂g */
       for (int k = 0; k < m; ++k) o[nn + 2 * nm + mm + n + k] = -ly[k];                    /* ∂h */
     }
+  } else if (j->jvp == 2) {
+    jacobian_z(d->family, n, m, fth, w->z, w->J);
+    int sing = 0;
+    j->out[b] = cond_estimate(N, w->J, w->rem, w->step, w->prow, w->JT, &sing);
+    failed = sing;
   } else {
     /* ForwardDiff Dual method, src/AutoDiff.jl:94-100: ż = −(∇F_z)⁻¹ ∇F_θ θ̇ per partial */
     for (int c = 0; c < j->K; ++c) {
@@ -1133,6 +1269,25 @@ int oracle_jvp_batch_nl(const mcpx_desc* d, const double* theta, const double* x
   memset(&j, 0, sizeof j);
   j.jvp = 1; j.d = d; j.theta = theta; j.x = x; j.y = y; j.s = s; j.nl = nl;
   j.tdot = theta_dot; j.K = n_partials; j.out = zdot; j.status = status;
+  return sens_run(&j, nthreads);
+}
+
+/* rcond [B] and status [B] (1: ∇F_z exactly singular) at the returned iterate (cond_estimate). */
+int oracle_cond_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                      const double* s, double* rcond, int32_t* status, int nthreads) {
+  if (!d) return MCPX_EINVAL;
+  sens_job j;
+  memset(&j, 0, sizeof j);
+  j.jvp = 2; j.d = d; j.theta = theta; j.x = x; j.y = y; j.s = s; j.out = rcond; j.status = status;
+  return sens_run(&j, nthreads);
+}
+
+int oracle_cond_batch_nl(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                         const double* s, double* rcond, int32_t* status, int nthreads, const oracle_nl* nl) {
+  if (!d || !nl || !nl->init || !nl->eval) return MCPX_EINVAL;
+  sens_job j;
+  memset(&j, 0, sizeof j);
+  j.jvp = 2; j.d = d; j.theta = theta; j.x = x; j.y = y; j.s = s; j.nl = nl; j.out = rcond; j.status = status;
   return sens_run(&j, nthreads);
 }
 

@@ -173,7 +173,8 @@ def test_gpu_band_t10(gpu, oracle_lib, B, warm):
     from tests.test_gpu_parity import assert_parity
 
     assert_parity(got, ref)
-    assert (ref["status"] == 0).mean() > 0.8
+    if not warm:  # the bench's θ from x₀ = 0 (the zero-input warm start solves fewer: parity only)
+        assert (ref["status"] == 0).mean() > 0.8
 
 
 @pytest.mark.gpu

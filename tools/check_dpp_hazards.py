@@ -26,6 +26,16 @@
    gfx9 table's EXEC-write → DPP distance, applied conservatively to SALU writes too, which
    the compiler cannot pad for when they sit inside asm).
 
+4. An MFMA result read by an inline-asm instruction too early.  A VALU, LDS, buffer/global
+   or export instruction reading a VGPR that `v_mfma_f64_16x16x4_f64` wrote needs 19
+   independent instructions in between (the dependency table of the CDNA3/4 ISA; LLVM's
+   DMFMA16x16WriteVgprVALUReadWaitStates / …MemExpReadWaitStates; 6 after the 4x4x4 DGEMM,
+   and 19 is taken for every other MFMA too).  hipcc pads this for its own instructions, not
+   for a consumer inside an asm string: the round-4 Gauss-Jordan that recorded pivot 0 by a
+   one-lane `ds_write_b64` of the accumulator right after the Schur MFMAs stored the register's
+   stale value, and every C3 instance came back a few ulps off.  The walk
+   stops at a label: the kernels' MFMA results are consumed in the block that computed them.
+
     python tools/check_dpp_hazards.py path/to/file.s [kernel-substring]
 Exit status 1 if any hazard is found.
 """
@@ -189,6 +199,68 @@ def wait_state_hazards(insts, want: str):
     return bad, checked
 
 
+MFMA_READ_STATES = {"v_mfma_f64_16x16x4": 19, "v_mfma_f64_4x4x4": 6}
+
+
+def mfma_need(op: str) -> int:
+    for k, v in MFMA_READ_STATES.items():
+        if op.startswith(k):
+            return v
+    return 19
+
+
+def asm_vgpr_reads(t: str) -> set:
+    """VGPRs an instruction reads: every operand of a store / DS write / export; the sources of a
+    VALU op (and its destination for the accumulating / partial writers)."""
+    op = t.split()[0]
+    ops = [x.strip() for x in t[len(op):].split(",")]
+    if op.startswith(("ds_write", "ds_store", "buffer_store", "global_store", "flat_store", "exp")):
+        return set().union(*(regs(x) for x in ops)) if ops else set()
+    if op.startswith(("ds_", "buffer_", "global_", "flat_")):  # loads: address operands only
+        return set().union(*(regs(x) for x in ops[1:])) if len(ops) > 1 else set()
+    if op.startswith("v_"):
+        rd = set().union(*(regs(x) for x in ops[1:])) if len(ops) > 1 else set()
+        if "fmac" in op or "_mac_" in op or op.startswith(("v_writelane", "v_permlane")):
+            rd |= regs(ops[0])
+        return rd
+    return set()
+
+
+def mfma_read_hazards(insts, want: str):
+    """4. An asm instruction reading an MFMA's destination VGPRs fewer than mfma_need() wait
+    states after the MFMA (same block)."""
+    bad, checked = [], 0
+    for i, (k, t, asm, lab) in enumerate(insts):
+        if not asm or lab or (want and want not in (k or "")):
+            continue
+        live = asm_vgpr_reads(t)
+        if not live:
+            continue
+        checked += 1
+        states, j = 0, i - 1
+        while j >= 0 and live and states < 19:
+            kk, tt, _, ll = insts[j]
+            if kk != k or ll:
+                break
+            o = tt.split()[0]
+            if o == "s_nop":
+                states += int(tt.split()[1], 0) + 1
+                j -= 1
+                continue
+            if o.startswith("v_mfma"):
+                hit = regs(tt[len(o):].split(",")[0]) & live
+                if hit and states < mfma_need(o):
+                    bad.append(f"MFMA-RESULT HAZARD in {k}:\n   {tt}\n   {t}  ({states} wait states between, "
+                               f"{mfma_need(o)} needed)")
+                    break
+                live -= hit
+            else:
+                live -= valu_dst(tt)
+            states += 1
+            j -= 1
+    return bad, checked
+
+
 def exec_switch_blocks(insts):
     """Start indices of asm blocks that save EXEC and set it (s_mov_b64 sX, exec;
     s_mov_b64 exec, sY), with the VGPRs their v_readfirstlane read."""
@@ -255,6 +327,9 @@ def main(argv=None):
     insts = parse(path)
     w, wc = wait_state_hazards(insts, want)
     w += exec_dpp_hazards(insts, want)
+    mf, mc = mfma_read_hazards(insts, want)
+    w += mf
+    wc += mc
     x, xc = narrowed_exec_hazards(insts, want)
     for msg in (w + x)[:50]:
         print(msg)

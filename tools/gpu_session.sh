@@ -10,6 +10,7 @@
 #   bench=<name>:<args>   one bench line, args comma-separated (bench=c4:--lane-change,2)
 #   prof=<name>:<args>    tools/gpu_profile.sh: bench line + rocprofv3 trace + PMC passes
 #   timeline=<args>       tools/timeline.py (residency timeline of a SCHUR launch), args comma-separated
+#   probe=<name>          tools/parity_probe.py (C3, C2 shapes) on the variant tools/ablib/libmcpx_<name>.so
 #   shard                 the per-GPU shards of the strong-scaling configs (C3 2/4/8, C5 512, C4 128)
 #
 # Outputs go to gpurun_out/<out-dir-name>/ (prof steps: gpurun_out/prof_<name>/).  Every GPU
@@ -21,6 +22,8 @@ shift
 mkdir -p "$O"
 export TMPDIR=/tmp
 T="--timeout 300 --timeout-method thread"
+# the tree must be built here, not on the box: a missing module would compile silently for minutes
+timeout -k 10 300 python tools/check_prebuilt.py || exit 2
 for step in "$@"; do
   echo "[gpu_session] $step $(date +%T)"
   case "$step" in
@@ -48,6 +51,12 @@ for step in "$@"; do
       args=${step#timeline=}
       timeout -k 10 300 python -u tools/timeline.py ${args//,/ } --out "$O" > "$O/timeline.log" 2>&1 || { tail -20 "$O/timeline.log"; exit 9; }
       cut -c1-600 "$O/timeline.log" ;;
+    probe=*)
+      lib=${step#probe=}
+      for shape in "32 16 256" "16 8 256"; do
+        MCPX_LIB_PATH=tools/ablib/libmcpx_$lib.so timeout -k 10 180 python tools/parity_probe.py $shape >> "$O/parity_probe.txt" 2>&1 || { tail -20 "$O/parity_probe.txt"; exit 10; }
+      done
+      tail -20 "$O/parity_probe.txt" ;;
     shard)
       for G in 32768 16384 8192; do
         timeout -k 10 300 python bench.py --gpus 1 --global-batch $G --steps 20 --warmup 5 --cpu-sample 0 --host-runs 0 > "$O/bench_g$G.json" 2> "$O/bench_g$G.err" || exit 8
