@@ -57,7 +57,7 @@ extern "C" {
  * struct's size and layout: a caller built against a 1.x header passes a shorter
  * struct, so the major version moved.  Callers check mcpx_version() / 10000 against
  * MCPX_VERSION / 10000 before the first call (mcp_amd/_lib.py does). */
-#define MCPX_VERSION 20000 /* 2.0.0 */
+#define MCPX_VERSION 20100 /* 2.1.0: mcpx_cond_batch* */
 
 /* error codes */
 #define MCPX_OK 0
@@ -290,6 +290,20 @@ int mcpx_solve_vjp_batch_device(const mcpx_desc* desc, const double* theta,
                                 const mcpx_cotangent* ct, double* dtheta,
                                 int32_t* vjp_status, void* stream);
 
+/* Conditioning of the pullback's matrix.  The reference's rrule solves with a column-pivoted QR
+ * of −∇F_z (src/AutoDiff.jl:39); at degenerate solutions ∇F_z is nearly singular and QR and LU
+ * sensitivities can differ at O(1).  rcond[b] = 1 / (‖∇F_z‖₁ · est‖∇F_z⁻¹‖₁) at (x, y, s), ∇F_z
+ * without tol·I: the Hager–Higham estimate (≤ 5 rounds of solves with the LU factors and
+ * their transpose, plus the alternating-sign lower bound), which never exceeds the true
+ * ‖∇F_z⁻¹‖₁, so rcond[b] ≥ 1 / cond₁(∇F_z).  status[b] = 1 and rcond[b] = 0: ∇F_z exactly
+ * singular.  A caller flags an instance as ill-conditioned when rcond[b] < its threshold
+ * (mcp_amd.batch.ILL_CONDITIONED = 1e-12: fewer than ~4 significant digits in the
+ * sensitivities).  Every size runs one workgroup per instance (n + 2m <= MCPX_MAX_WG_KKT_DIM). */
+int mcpx_cond_batch(const mcpx_desc* desc, const double* theta, const double* x, const double* y,
+                    const double* s, int num_devices, double* rcond, int32_t* status);
+int mcpx_cond_batch_device(const mcpx_desc* desc, const double* theta, const double* x, const double* y,
+                           const double* s, double* rcond, int32_t* status, void* stream);
+
 /* Forward mode — the ForwardDiff.Dual method of solve (src/AutoDiff.jl:84-117):
  *     ż_c = (∂z/∂θ) θ̇_c = −(∇F_z)⁻¹ (∇F_θ θ̇_c),   c = 0 .. n_partials−1.
  * theta_dot [B*n_partials*p] (instance-major, then partial-major, stride p);
@@ -366,6 +380,11 @@ int mcpx_jvp_batch_module(mcpx_module* mod, const mcpx_desc* desc, const double*
 int mcpx_jvp_batch_module_device(mcpx_module* mod, const mcpx_desc* desc, const double* theta,
                                  const double* x, const double* y, const double* s, int32_t n_partials,
                                  const double* theta_dot, double* zdot, int32_t* status, void* stream);
+int mcpx_cond_batch_module(mcpx_module* mod, const mcpx_desc* desc, const double* theta, const double* x,
+                           const double* y, const double* s, int num_devices, double* rcond, int32_t* status);
+int mcpx_cond_batch_module_device(mcpx_module* mod, const mcpx_desc* desc, const double* theta,
+                                  const double* x, const double* y, const double* s, double* rcond,
+                                  int32_t* status, void* stream);
 
 #ifdef __cplusplus
 }

@@ -30,7 +30,8 @@ EXPORTS = ("mcpx_version", "mcpx_last_error", "mcpx_default_params", "mcpx_theta
            "mcpx_vjp_batch_device", "mcpx_jvp_batch", "mcpx_jvp_batch_device", "mcpx_module_load",
            "mcpx_module_dims", "mcpx_module_unload", "mcpx_solve_batch_module", "mcpx_solve_batch_module_device",
            "mcpx_host_register", "mcpx_host_unregister", "mcpx_vjp_batch_module", "mcpx_vjp_batch_module_device",
-           "mcpx_jvp_batch_module", "mcpx_jvp_batch_module_device", "mcpx_solve_vjp_batch_device")
+           "mcpx_jvp_batch_module", "mcpx_jvp_batch_module_device", "mcpx_solve_vjp_batch_device",
+           "mcpx_cond_batch", "mcpx_cond_batch_device", "mcpx_cond_batch_module", "mcpx_cond_batch_module_device")
 
 
 ABI_MAJOR = 2  # include/mcpx.h MCPX_VERSION / 10000
@@ -94,6 +95,14 @@ def lib():
     L.mcpx_jvp_batch_module_device.restype = C.c_int
     L.mcpx_jvp_batch_module_device.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P, C.c_int32, P, P, P,
                                                P]
+    L.mcpx_cond_batch.restype = C.c_int
+    L.mcpx_cond_batch.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, C.c_int, P, P]
+    L.mcpx_cond_batch_device.restype = C.c_int
+    L.mcpx_cond_batch_device.argtypes = [C.POINTER(_abi.Desc), P, P, P, P, P, P, P]
+    L.mcpx_cond_batch_module.restype = C.c_int
+    L.mcpx_cond_batch_module.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P, C.c_int, P, P]
+    L.mcpx_cond_batch_module_device.restype = C.c_int
+    L.mcpx_cond_batch_module_device.argtypes = [C.c_void_p, C.POINTER(_abi.Desc), P, P, P, P, P, P, P]
     L.mcpx_host_register.restype = C.c_int
     L.mcpx_host_register.argtypes = [C.c_void_p, C.c_size_t]
     L.mcpx_host_unregister.restype = C.c_int

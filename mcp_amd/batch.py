@@ -251,6 +251,31 @@ def jvp_batch(family: int, n: int, m: int, theta, x, y, s, theta_dot, num_device
     return zd, st
 
 
+# rcond below which an instance's sensitivities count as ill-conditioned (include/mcpx.h
+# mcpx_cond_batch): cond₁(∇F_z) > 1e12 leaves fewer than ~4 significant digits in ∂z/∂θ
+ILL_CONDITIONED = 1e-12
+
+
+def cond_batch(family: int, n: int, m: int, theta, x, y, s, num_devices: int = 0,
+               module: Module | None = None) -> tuple:
+    """Reciprocal 1-norm condition estimate of ∇F_z at the solutions (the matrix of the rrule's
+    solve, src/AutoDiff.jl:39) on the GPU(s) → (rcond (B,), status (B,): 1 = exactly singular).
+    `rcond < ILL_CONDITIONED` is the per-instance ill-conditioning flag."""
+    theta = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+    B, ld = theta.shape
+    x, y, s = _host_f64(x, (B, n)), _host_f64(y, (B, m)), _host_f64(s, (B, m))
+    rc = np.empty(B)
+    st = np.empty(B, np.int32)
+    desc = _abi.Desc(int(family), int(n), int(m), 0, int(B), int(ld))
+    if module is not None:
+        check(lib().mcpx_cond_batch_module(module.handle, C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s),
+                                           int(num_devices), _ptr(rc), _ptr(st)))
+    else:
+        check(lib().mcpx_cond_batch(C.byref(desc), _ptr(theta), _ptr(x), _ptr(y), _ptr(s), int(num_devices),
+                                    _ptr(rc), _ptr(st)))
+    return rc, st
+
+
 def _dev_f64(t, what):
     import torch
 

@@ -723,7 +723,8 @@ int launch_sens_wg_impl(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, const Se
   const int n = d->n, m = d->m, N = n + 2 * m, nr = n + m;
   const int ns = jvp ? N : nr;
   const int K = a.n_partials;
-  const int nrhs = jvp ? std::max(1, std::min(K, MCPX_JVP_RHS)) : 1;
+  // (the condition estimate: two N-vectors of scratch in the right-hand-side area)
+  const int nrhs = a.mode == 1 ? 2 : (jvp ? std::max(1, std::min(K, MCPX_JVP_RHS)) : 1);
   hipFunction_t f = nullptr;
   const void* kp = nullptr;
   int per_cu = 0;
@@ -774,7 +775,7 @@ int launch_sens_wg_impl(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, const Se
     w.s.gy = a.gy ? a.gy + b0 * m : nullptr;
     w.s.gs = a.gs ? a.gs + b0 * m : nullptr;
     w.s.theta_dot = a.theta_dot ? a.theta_dot + b0 * K * a.p : nullptr;
-    w.s.out = a.out + (jvp ? b0 * K * N : b0 * a.p);
+    w.s.out = a.out + (a.mode == 1 ? b0 : (jvp ? b0 * K * N : b0 * a.p));
     w.s.status = a.status ? a.status + b0 : nullptr;
     w.batch = nb;
     hipError_t e = hipMemsetAsync(w.counter, 0, sizeof(int32_t), st);
@@ -851,7 +852,7 @@ int sens_shard(bool jvp, int dev, const mcpx_desc* d, const mcpx::SensArgs& a0, 
   HIP_TRY(up(dx, x, n)); HIP_TRY(up(dy, y, m)); HIP_TRY(up(ds, s, m));
   HIP_TRY(up(dgx, gx, n)); HIP_TRY(up(dgy, gy, m)); HIP_TRY(up(dgs, gs, m));
   HIP_TRY(up(dtd, tdot, (size_t)K * p));
-  const size_t per_out = jvp ? (size_t)K * N : (size_t)p;
+  const size_t per_out = a0.mode == 1 ? 1 : (jvp ? (size_t)K * N : (size_t)p);
   HIP_TRY(dout.alloc((size_t)nb * per_out));
   if (status) HIP_TRY(dst.alloc(nb));
   mcpx_desc dd = *d;
@@ -979,6 +980,44 @@ int jvp_host_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, con
   if (n_partials > 0 && !theta_dot) return fail(MCPX_EINVAL, "theta_dot is NULL");
   return sens_host(true, d, a, plan, theta, x, y, s, nullptr, nullptr, nullptr, theta_dot, num_devices, zdot,
                    status);
+}
+
+// mcpx_cond_batch*: the JVP workgroup kernels in their condition-estimate mode (every size and
+// family runs the workgroup layout: the estimate's solves reuse the factors in the slot).
+int prepare_cond(const mcpx_desc* d, mcpx::SensArgs* a, SensPlan* plan, mcpx_module* mod) {
+  int rc = prepare_sens(d, a, plan, true, mod);
+  if (rc) return rc;
+  if (!plan->wg) {
+    plan->wg = true;
+    plan->nv = pick_wg_bucket(d->n + 2 * d->m);
+  }
+  a->mode = 1;
+  return MCPX_OK;
+}
+
+int cond_device_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                     const double* s, double* rcond, int32_t* status, void* stream) {
+  mcpx::SensArgs a;
+  SensPlan plan;
+  int rc;
+  if ((rc = prepare_cond(d, &a, &plan, mod))) return rc;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, rcond))) return rc;
+  int dev = 0;
+  if ((rc = current_device(&dev))) return rc;
+  return launch_sens(true, d, a, plan, theta, x ? x : theta, y ? y : theta, s ? s : theta, nullptr, nullptr,
+                     nullptr, nullptr, rcond, status, (hipStream_t)stream);
+}
+
+int cond_host_impl(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                   const double* s, int num_devices, double* rcond, int32_t* status) {
+  mcpx::SensArgs a;
+  SensPlan plan;
+  int rc;
+  if ((rc = prepare_cond(d, &a, &plan, mod))) return rc;
+  if (d->batch == 0) return MCPX_OK;
+  if ((rc = sens_inputs_ok(d, theta, x, y, s, rcond))) return rc;
+  return sens_host(true, d, a, plan, theta, x, y, s, nullptr, nullptr, nullptr, nullptr, num_devices, rcond, status);
 }
 
 // mcpx_solve_batch_device / mcpx_solve_batch_module_device (mod = nullptr: QP / affine kernels).
@@ -1163,6 +1202,28 @@ int mcpx_jvp_batch_device(const mcpx_desc* d, const double* theta, const double*
 int mcpx_jvp_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y, const double* s,
                    int32_t n_partials, const double* theta_dot, int num_devices, double* zdot, int32_t* status) {
   return jvp_host_impl(nullptr, d, theta, x, y, s, n_partials, theta_dot, num_devices, zdot, status);
+}
+
+int mcpx_cond_batch(const mcpx_desc* d, const double* theta, const double* x, const double* y, const double* s,
+                    int num_devices, double* rcond, int32_t* status) {
+  return cond_host_impl(nullptr, d, theta, x, y, s, num_devices, rcond, status);
+}
+
+int mcpx_cond_batch_device(const mcpx_desc* d, const double* theta, const double* x, const double* y,
+                           const double* s, double* rcond, int32_t* status, void* stream) {
+  return cond_device_impl(nullptr, d, theta, x, y, s, rcond, status, stream);
+}
+
+int mcpx_cond_batch_module(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x,
+                           const double* y, const double* s, int num_devices, double* rcond, int32_t* status) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  return cond_host_impl(mod, d, theta, x, y, s, num_devices, rcond, status);
+}
+
+int mcpx_cond_batch_module_device(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x,
+                                  const double* y, const double* s, double* rcond, int32_t* status, void* stream) {
+  if (!mod) return fail(MCPX_EINVAL, "module is NULL");
+  return cond_device_impl(mod, d, theta, x, y, s, rcond, status, stream);
 }
 
 int mcpx_vjp_batch_module(mcpx_module* mod, const mcpx_desc* d, const double* theta, const double* x,

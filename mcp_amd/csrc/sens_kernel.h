@@ -26,6 +26,8 @@ struct SensArgs {
   int32_t n, m;
   int32_t n_partials;       // K (JVP)
   int32_t family;
+  int32_t mode;             // workgroup JVP kernels: 1 = condition estimate (out = rcond [B], mcpx_cond_batch)
+  int32_t pad_;
   // VJP cotangent g = a ⊙ z + b per block (b = gx / gy / gs above, NULL = 0): a = 0 is the
   // plain cotangent arrays; a ≠ 0 the gradient of a separable quadratic loss
   // l = Σ ½ a z² + b·z (e.g. a = 2, b = 0: f = Σx² + Σy², test/runtests.jl:72-75),

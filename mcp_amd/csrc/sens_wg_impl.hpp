@@ -11,6 +11,8 @@
 //  * JVP — the ForwardDiff.Dual method (src/AutoDiff.jl:84-117): ∇F_z ż = −∇F_θ θ̇
 //    on the full (n+2m)-dim ∇F_z, `nrhs` partials per factorisation (each a trailing
 //    column of the same elimination: the oracle's per-partial lu_solve bit for bit).
+//  * condition estimate (SensArgs::mode = 1, the JVP kernels: mcpx_cond_batch) — rcond of
+//    ∇F_z by the Hager–Higham 1-norm estimate from one LU (cond_one below).
 // The system [K | rhs] is written into the slot's HBM workspace and factored by
 // wg::lu_solve (blocked LU with partial pivoting, MFMA trailing update).  Entries,
 // right-hand sides and the ∂θ contraction follow oracle/ipm_oracle.c sens_one op for
@@ -117,6 +119,144 @@ __device__ __forceinline__ double dtheta_entry(int64_t t, const double* lam, con
   }
 }
 
+// ---- condition estimate of ∇F_z (oracle/ipm_oracle.c cond_estimate, op for op) -------------
+// After lu_solve with no right-hand side, row i of A holds the multipliers l_ik (k < step(i))
+// and u_ik (k ≥ step(i)); L.prow / L.step_of give the pivot order.  Solves are column-oriented,
+// one barrier per step (each thread owns the rows i ≡ tid mod 256); the short sequential parts
+// (sums, sign vector, argmax) run on thread 0 in the oracle's order.
+
+// A x = b: b (row-indexed) destroyed, x (column-indexed).
+template <int NSMAX>
+__device__ __forceinline__ void lu_apply(const double* __restrict__ A, int ld, int N, const LuShared<NSMAX>& L,
+                                         double* b, double* x) {
+  const int tid = threadIdx.x;
+  for (int k = 0; k < N; ++k) {
+    const double bp = b[L.prow[k]];
+    for (int i = tid; i < N; i += WG)
+      if (L.step_of[i] > k) b[i] = fma(-A[(int64_t)i * ld + k], bp, b[i]);
+    __syncthreads();
+  }
+  for (int k = N - 1; k >= 0; --k) {
+    const int p = L.prow[k];
+    const double xk = b[p] / A[(int64_t)p * ld + k];
+    if (tid == 0) x[k] = xk;
+    for (int i = tid; i < N; i += WG)
+      if (L.step_of[i] < k) b[i] = fma(-A[(int64_t)i * ld + k], xk, b[i]);
+    __syncthreads();
+  }
+}
+
+// Aᵀ z = c (PA = LU): c (column-indexed) destroyed, u (N scratch), z (row-indexed).
+template <int NSMAX>
+__device__ __forceinline__ void lu_apply_t(const double* __restrict__ A, int ld, int N, const LuShared<NSMAX>& L,
+                                           double* c, double* u, double* z) {
+  const int tid = threadIdx.x;
+  for (int k = 0; k < N; ++k) {  // Uᵀ
+    const double* ur = A + (int64_t)L.prow[k] * ld;
+    const double uk = c[k] / ur[k];
+    if (tid == 0) u[k] = uk;
+    for (int i = k + 1 + tid; i < N; i += WG) c[i] = fma(-ur[i], uk, c[i]);
+    __syncthreads();
+  }
+  for (int k = N - 1; k >= 0; --k) {  // Lᵀ
+    const double* lr = A + (int64_t)L.prow[k] * ld;
+    const double vk = u[k];
+    for (int j = tid; j < k; j += WG) u[j] = fma(-lr[j], vk, u[j]);
+    if (tid == 0) z[L.prow[k]] = vk;
+    __syncthreads();
+  }
+}
+
+// rcond of the N×N ∇F_z in A (destroyed); v0..v2: LDS vectors, h: 2·N doubles of HBM scratch.
+template <int NSMAX>
+__device__ __forceinline__ double cond_one(double* __restrict__ A, int ld, int N, LuShared<NSMAX>& L, double* v0,
+                                           double* v1, double* v2, double* h, double* xs, Scratch& sc, bool& singular) {
+  const int tid = threadIdx.x;
+  for (int j = tid; j < N; j += WG) {  // column sums of |a_ij|, rows ascending
+    double c = 0.0;
+    for (int i = 0; i < N; ++i) c = c + fabs(A[(int64_t)i * ld + j]);
+    h[j] = c;
+  }
+  __syncthreads();
+  double anorm = 0.0;  // (thread 0's value is the one used)
+  if (tid == 0) {
+    for (int j = 0; j < N; ++j) {
+      const double c = h[j];
+      if (c > anorm || c != c) anorm = c;
+      if (anorm != anorm) break;
+    }
+  }
+  __syncthreads();
+  singular = !lu_solve<NSMAX>(A, ld, N, xs, L, 0, nullptr);
+  if (singular) return 0.0;
+  double* const x = v0;   // the rhs of the next solve (destroyed by it)
+  double* const y = v1;   // A⁻¹x
+  double* const xi = v2;  // sign(y) of the previous round
+  double* const z = h;    // A⁻ᵀξ
+  double* const u = h + N;
+  const double inv = 1.0 / (double)N;
+  for (int i = tid; i < N; i += WG) x[i] = inv;
+  __syncthreads();
+  double est = 0.0;  // thread 0 holds the estimate; the stop decisions go through sc.i[0]
+  int jprev = -1;
+  for (int it = 0; it < 5; ++it) {
+    lu_apply<NSMAX>(A, ld, N, L, x, y);
+    if (tid == 0) {
+      double g = 0.0;
+      for (int k = 0; k < N; ++k) g = g + fabs(y[k]);
+      int stop = it > 0 && !(g > est);
+      if (!stop) {
+        est = g;
+        int same = it > 0;
+        for (int k = 0; k < N; ++k) {
+          const double sg = y[k] >= 0.0 ? 1.0 : -1.0;
+          if (sg != xi[k]) same = 0;
+          xi[k] = sg;
+        }
+        stop = same;
+      }
+      sc.i[0] = stop;
+    }
+    __syncthreads();
+    if (sc.i[0]) break;
+    for (int k = tid; k < N; k += WG) x[k] = xi[k];
+    __syncthreads();
+    lu_apply_t<NSMAX>(A, ld, N, L, x, u, z);
+    if (tid == 0) {
+      int jm = -1;
+      double bz = -1.0;
+      for (int i = 0; i < N; ++i)
+        if (fabs(z[i]) > bz) {
+          bz = fabs(z[i]);
+          jm = i;
+        }
+      if (jm < 0) jm = 0;
+      const int stop = it > 0 && !(fabs(z[jm]) > z[jprev]);
+      if (!stop) jprev = jm;
+      sc.i[0] = stop;
+      sc.i[1] = jm;
+    }
+    __syncthreads();
+    if (sc.i[0]) break;
+    const int jm = sc.i[1];
+    for (int i = tid; i < N; i += WG) x[i] = i == jm ? 1.0 : 0.0;
+    __syncthreads();
+  }
+  for (int i = tid; i < N; i += WG) x[i] = (i & 1 ? -1.0 : 1.0) * (1.0 + (N > 1 ? (double)i / (double)(N - 1) : 0.0));
+  __syncthreads();
+  lu_apply<NSMAX>(A, ld, N, L, x, y);
+  double rc = 0.0;
+  if (tid == 0) {
+    double g = 0.0;
+    for (int k = 0; k < N; ++k) g = g + fabs(y[k]);
+    const double alt = 2.0 * g / (3.0 * (double)N);
+    if (alt > est) est = alt;
+    const double den = anorm * est;
+    rc = (den > 0.0 && den <= __DBL_MAX__) ? 1.0 / den : 0.0;
+  }
+  return rc;  // thread 0's
+}
+
 template <int FAMILY, bool JVP, int NVMAX, int NSMAX, class GEN>
 __device__ __forceinline__ void sens_instances(const WgSensArgs& W) {
   constexpr bool NL = FAMILY == MCPX_FAMILY_NONLINEAR;
@@ -161,6 +301,22 @@ __device__ __forceinline__ void sens_instances(const WgSensArgs& W) {
       }
     }
     __syncthreads();
+
+    if constexpr (JVP) {
+      if (a.mode == 1) {  // mcpx_cond_batch: rcond of ∇F_z at the returned iterate
+        for (int r = wave; r < N; r += NWAVE)
+          for (int j = lane; j < N; j += 64) Am[(int64_t)r * ld + j] = jac<FAMILY, GEN>(th, blk, zs, n, m, r, j);
+        __syncthreads();
+        bool sing = false;
+        const double rc = cond_one<NSMAX>(Am, ld, N, S.lu, S.zs, S.Fs, S.dzs, sol, xs, S.sc, sing);
+        if (tid == 0) {
+          a.out[inst] = rc;
+          if (a.status) a.status[inst] = sing ? 1 : 0;
+        }
+        __syncthreads();
+        continue;
+      }
+    }
 
     bool ok_all = true;
     for (int c0 = 0; c0 < K; c0 += W.nrhs) {
