@@ -668,7 +668,7 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     p = theta_host.shape[1]
     rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
                   B * (8.0 * (p + n + 2 * m + 2) + 12.0), ev,
-                  "ipm_solve_kernel" if one_wave(n, m, ls) else "ipm_wg_kernel_t",
+                  "ipm_solve_kernel" if one_wave(n, m, ls) else "ipm_wg",  # ipm_wg_kernel_t / ipm_wg_vr_kernel_t
                   roofline_bound(ev, kern_ms, "valu" if one_wave(n, m, ls) else "hbm"),
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system, 2N^3/3+2N^2 per "
                   f"Newton step) x rank 0's own Newton counts / HIP-event time of the solve launch; executed = the FP64 "
