@@ -77,6 +77,9 @@
 #endif
 
 // Dispatch-order priority levels (A/B knob; 0 = off): see ipm_solve_kernel.
+#ifndef MCPX_AFF_LDS_R
+#define MCPX_AFF_LDS_R 1
+#endif
 #ifndef MCPX_PRIO
 #define MCPX_PRIO 0
 #endif
@@ -1164,7 +1167,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   // the same kernel with R in A's place and the G-side coupling −Qᵀ, with −h and −g, in
   // the wave's LDS (sQ, odd stride) — Q is column-major in θ, so its rows are strided there.
   constexpr bool AFF = SCH && FAMILY == MCPX_FAMILY_AFFINE;
-  constexpr bool LDSA = SCH && !AFF && NC > 0 && MC > 0 && MCPX_LDS_A;
+  // (MCPX_AFF_LDS_R: the affine kernel's R in LDS too, in A's slot — more LDS per wave)
+  constexpr bool LDSA = SCH && (!AFF || MCPX_AFF_LDS_R) && NC > 0 && MC > 0 && MCPX_LDS_A;
   constexpr int LDA = LDSA ? MC + 1 : 1;
   __shared__ double sA[LDSA ? NC * LDA + MC + NC : 1];
   constexpr bool LDSM = LDSA && NC <= 16 && MCPX_LDS_M;  // M (column-major, as in θ) in LDS too
@@ -1203,10 +1207,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   }
 
   if constexpr (LDSA) {  // read before the first step's barrier
-    const double* tg = th0 + NC * NC;
+    const double* tg = th0 + NC * NC + (AFF ? NC * MC : 0);  // A | the affine R
 #pragma unroll
     for (int i = lane; i < NC * MC; i += 64) sA[(i / MC) * LDA + i % MC] = tg[i];
-    for (int i = lane; i < MC + NC; i += 64) sA[NC * LDA + i] = tg[NC * MC + i];
+    if constexpr (!AFF)
+      for (int i = lane; i < MC + NC; i += 64) sA[NC * LDA + i] = tg[NC * MC + i];
   }
   if constexpr (LDSM) {
 #pragma unroll

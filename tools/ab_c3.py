@@ -18,12 +18,18 @@ ap.add_argument("--n", type=int, default=32)
 ap.add_argument("--m", type=int, default=16)
 ap.add_argument("--solver", default="schur")
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--family", default="qp", choices=["qp", "affine"], help="affine: the QPs as affine-family data")
 a = ap.parse_args()
 lib = os.environ.get("MCPX_LIB_PATH", "default")
 for B in a.batch:
-    th = torch.from_numpy(generate_global_slice(1, a.n, a.m, 0.0, 0, B)).cuda()
+    fam = 1 if a.family == "affine" else 0
+    thh = generate_global_slice(1, a.n, a.m, 0.0, 0, B)
+    if fam:
+        from mcp_amd.qp_benchmark import affine_embedding
+        thh = affine_embedding(thh, a.n, a.m)
+    th = torch.from_numpy(thh).cuda()
     out = alloc_device_outputs(B, a.n, a.m, th.device)
-    run = lambda: solve_batch_device(0, a.n, a.m, th, out, tol=1e-6, linear_solver=a.solver)
+    run = lambda: solve_batch_device(fam, a.n, a.m, th, out, tol=1e-6, linear_solver=a.solver)
     run(); torch.cuda.synchronize()
     ms = []
     for _ in range(a.reps):
@@ -34,5 +40,5 @@ for B in a.batch:
     for k in sorted(out):
         if out[k] is not None:
             h.update(out[k].cpu().numpy().tobytes())
-    print(json.dumps({"lib": os.path.basename(lib), "B": B, "ms_median": float(np.median(ms)), "ms_min": min(ms),
+    print(json.dumps({"lib": os.path.basename(lib), "family": a.family, "B": B, "ms_median": float(np.median(ms)), "ms_min": min(ms),
                       "solves_per_s": B / (np.median(ms) * 1e-3), "digest": h.hexdigest()[:16]}), flush=True)
