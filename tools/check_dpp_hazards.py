@@ -110,8 +110,12 @@ def valu_dst(t: str) -> set:
 
 
 def exec_dpp_hazards(insts, want: str):
-    """3. A DPP instruction fewer than 5 wait states after an EXEC write inside inline asm
-    (the EXEC switch of a broadcast): conservative, the compiler cannot pad for the asm's."""
+    """3. A DPP instruction fewer than 5 wait states after an EXEC write: an EXEC write inside
+    inline asm before any DPP (the EXEC switch of a broadcast; the compiler cannot pad for the
+    asm's), or any EXEC write — the compiler's restore after a divergent `if` included — before a
+    DPP inside asm (the compiler pads its own DPP, not an asm one).  The band kernel's DPP
+    variant (r05) lost lanes this way: `if (lane == p) {…}` ended with `s_or_b64 exec` two
+    instructions before the asm `v_fmac_f64_dpp`, which then ran under the narrowed EXEC."""
     bad = []
     for i, (k, t, asm, lab) in enumerate(insts):
         if lab or "_dpp" not in t.split()[0] or (want and want not in (k or "")):
@@ -126,7 +130,7 @@ def exec_dpp_hazards(insts, want: str):
                 states += int(tt.split()[1], 0) + 1
                 j -= 1
                 continue
-            if a and re.match(r"s_\S+\s+exec\b", tt):
+            if (a or asm) and re.match(r"s_\S+\s+exec\b", tt):
                 bad.append(f"EXEC→DPP HAZARD in {k}:\n   {tt}\n   {t}  ({states} wait states between)")
                 break
             states += 1
