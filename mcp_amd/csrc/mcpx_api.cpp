@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
 #include <map>
 #include <memory>
@@ -282,7 +283,8 @@ void set_chunk(mcpx::KernelArgs& a, const mcpx_desc* d, const double* theta, con
   a.fail_reason = o->fail_reason ? o->fail_reason + b0 : nullptr;
 }
 
-hipError_t pool_malloc(void** p, size_t bytes, hipStream_t st);  // the library's own pool (below)
+hipError_t dev_alloc(void** p, size_t bytes, hipStream_t st);  // the library's block cache (below)
+void dev_release(void* p, hipStream_t st);
 
 // Workgroup-per-instance launch (ipm_wg_impl.hpp): a persistent grid of the
 // resident workgroups pulls instances from an atomic counter; each workgroup
@@ -319,7 +321,7 @@ int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const d
   const int64_t grid_max = std::min(slots_max, std::min(CH, d->batch));
   double* ws = nullptr;
   const size_t bytes = sizeof(double) * (size_t)(grid_max * w.slot_stride) + 256;
-  HIP_TRY(pool_malloc((void**)&ws, bytes, st));
+  HIP_TRY(dev_alloc((void**)&ws, bytes, st));
   w.work = ws;
   w.counter = (int32_t*)(ws + grid_max * w.slot_stride);
   int rc = MCPX_OK;
@@ -340,7 +342,7 @@ int launch_wg(const mcpx_desc* d, const double* theta, const double* x0, const d
     }
     if (e != hipSuccess) rc = fail(MCPX_EHIP, "workgroup solver launch failed: %s", hipGetErrorString(e));
   }
-  HIP_TRY(hipFreeAsync(ws, st));
+  dev_release(ws, st);
   return rc;
 }
 
@@ -364,7 +366,7 @@ int launch_band(const mcpx_desc* d, const double* theta, const double* x0, const
   const int64_t stride = ((int64_t)mod->meta[9] + 31) / 32 * 32;
   const int64_t grid_max = std::min(slots_max, std::min((int64_t)1 << 30, d->batch));
   double* ws = nullptr;
-  HIP_TRY(pool_malloc((void**)&ws, sizeof(double) * (size_t)(grid_max * stride) + 256, st));
+  HIP_TRY(dev_alloc((void**)&ws, sizeof(double) * (size_t)(grid_max * stride) + 256, st));
   int32_t* counter = (int32_t*)(ws + grid_max * stride);
   mcpx::wg::WgArgs w{};
   w.counter = counter;
@@ -384,7 +386,7 @@ int launch_band(const mcpx_desc* d, const double* theta, const double* x0, const
     }
     if (e != hipSuccess) rc = fail(MCPX_EHIP, "band solver launch failed: %s", hipGetErrorString(e));
   }
-  HIP_TRY(hipFreeAsync(ws, st));
+  dev_release(ws, st);
   return rc;
 }
 
@@ -418,63 +420,113 @@ bool outputs_ok(const mcpx_out* o) {
          o->trace_len >= 0;
 }
 
-template <class T>
-struct DevBuf {
-  T* p = nullptr;
-  ~DevBuf() { if (p) (void)hipFree(p); }
-  hipError_t alloc(size_t count) { return count ? hipMalloc(&p, count * sizeof(T)) : hipSuccess; }
+// Library-internal device buffers: a per-device cache of hipMalloc'd blocks, never unmapped.
+// A block goes back to the cache with an event recorded on the stream of its last use; the
+// next user (any stream of that device) takes it after a stream wait on that event, so reuse
+// stays stream-ordered without host synchronisation.  (HIP 7.2's stream-ordered pools —
+// hipMallocFromPoolAsync / hipFreeAsync, whose default VM heap remaps recycled memory — gave
+// wrong answers here: from the fourth back-to-back host call on, ~15 of 1,024 T = 10 games
+// every other call, with torch's bundled HIP 7.0 runtime or DEBUG_HIP_MEM_POOL_VMHEAP=0
+// never; tools/band_stress.py)  Idle blocks beyond kCacheKeep bytes per
+// device are freed once their last use has completed; the cache lives for the process (no
+// HIP calls during teardown).
+constexpr uint64_t kCacheKeep = 4ull << 30;
+
+struct Block {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipEvent_t last = nullptr;  // recorded after the block's last use
+  bool busy = false;
 };
 
-// Device allocations of the host-buffer path and the workgroup kernels' workspaces come
-// from the library's own stream-ordered pool per device (hipMemPoolCreate).  Freed blocks
-// stay in it for the next call up to kPoolKeep bytes (its release threshold: the caching a
-// long-lived handle would give, bounded), and the device's default pool — shared with torch
-// and every other allocator in the process — keeps its own attributes.  The pools live for
-// the process (no HIP calls during teardown).
-constexpr uint64_t kPoolKeep = 4ull << 30;
+struct BlockCache {
+  std::mutex mu;
+  std::map<int, std::vector<Block>> dev;  // device → blocks
+};
 
-int lib_pool(int dev, hipMemPool_t* out) {
-  static std::mutex mu;
-  static std::map<int, hipMemPool_t> pools;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = pools.find(dev);
-  if (it != pools.end()) {
-    *out = it->second;
-    return MCPX_OK;
-  }
-  hipMemPoolProps props;
-  std::memset(&props, 0, sizeof props);
-  props.allocType = hipMemAllocationTypePinned;
-  props.location.type = hipMemLocationTypeDevice;
-  props.location.id = dev;
-  hipMemPool_t pool;
-  HIP_TRY(hipMemPoolCreate(&pool, &props));
-  uint64_t keep = kPoolKeep;
-  HIP_TRY(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
-  pools[dev] = pool;
-  *out = pool;
-  return MCPX_OK;
+BlockCache& block_cache() {
+  static BlockCache* c = new BlockCache;  // never destroyed
+  return *c;
 }
 
-// Stream-ordered allocation from the library pool of the current device.
-hipError_t pool_malloc(void** p, size_t bytes, hipStream_t st) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
+hipError_t dev_alloc(void** p, size_t bytes, hipStream_t st) {
+  *p = nullptr;
+  int d = 0;
+  hipError_t e = hipGetDevice(&d);
   if (e != hipSuccess) return e;
-  hipMemPool_t pool;
-  if (lib_pool(dev, &pool) != MCPX_OK) return hipErrorOutOfMemory;
-  return hipMallocFromPoolAsync(p, bytes, pool, st);
+  const size_t want = (std::max<size_t>(bytes, 1) + (2u << 20) - 1) / (2u << 20) * (2u << 20);  // 2 MiB granules
+  BlockCache& c = block_cache();
+  std::lock_guard<std::mutex> lock(c.mu);
+  auto& v = c.dev[d];
+  Block* best = nullptr;  // the smallest idle block that fits without wasting more than half of it
+  for (auto& b : v)
+    if (!b.busy && b.bytes >= want && b.bytes <= 2 * want && (!best || b.bytes < best->bytes)) best = &b;
+  if (best) {
+    if (best->last && (e = hipStreamWaitEvent(st, best->last, 0)) != hipSuccess) return e;
+    best->busy = true;
+    *p = best->p;
+    return hipSuccess;
+  }
+  Block b;
+  b.bytes = want;
+  if ((e = hipMalloc(&b.p, want)) != hipSuccess) {
+    // out of memory: free the idle blocks (after their last use) and try once more
+    for (auto it = v.begin(); it != v.end();) {
+      if (it->busy) { ++it; continue; }
+      if (it->last) (void)hipEventSynchronize(it->last), (void)hipEventDestroy(it->last);
+      (void)hipFree(it->p);
+      it = v.erase(it);
+    }
+    (void)hipGetLastError();
+    if ((e = hipMalloc(&b.p, want)) != hipSuccess) return e;
+  }
+  b.busy = true;
+  v.push_back(b);
+  *p = b.p;
+  return hipSuccess;
+}
+
+void dev_release(void* p, hipStream_t st) {
+  if (!p) return;
+  BlockCache& c = block_cache();
+  std::lock_guard<std::mutex> lock(c.mu);
+  for (auto& [d, v] : c.dev) {
+    for (auto& b : v) {
+      if (b.p != p) continue;
+      if (!b.last) (void)hipEventCreateWithFlags(&b.last, hipEventDisableTiming);
+      if (b.last) (void)hipEventRecord(b.last, st);
+      b.busy = false;
+      uint64_t idle = 0;  // trim: idle bytes beyond kCacheKeep, oldest first, once completed
+      for (auto& q : v) idle += q.busy ? 0 : q.bytes;
+      for (auto it = v.begin(); it != v.end() && idle > kCacheKeep;) {
+        if (it->busy || it->p == p || (it->last && hipEventQuery(it->last) != hipSuccess)) { ++it; continue; }
+        idle -= it->bytes;
+        if (it->last) (void)hipEventDestroy(it->last);
+        (void)hipFree(it->p);
+        it = v.erase(it);
+      }
+      (void)d;
+      return;
+    }
+  }
 }
 
 template <class T>
-struct AsyncBuf {  // stream-ordered device buffer, freed on the stream it was allocated on
+struct DevBuf {  // a cache block used on the null stream (synchronous callers)
+  T* p = nullptr;
+  ~DevBuf() { dev_release(p, nullptr); }
+  hipError_t alloc(size_t count) { return count ? dev_alloc((void**)&p, count * sizeof(T), nullptr) : hipSuccess; }
+};
+
+template <class T>
+struct AsyncBuf {  // a cache block, released on the stream it was allocated on
   T* p = nullptr;
   hipStream_t st = nullptr;
   hipError_t alloc(size_t count, hipStream_t s) {
     st = s;
-    return count ? pool_malloc((void**)&p, count * sizeof(T), s) : hipSuccess;
+    return count ? dev_alloc((void**)&p, count * sizeof(T), s) : hipSuccess;
   }
-  ~AsyncBuf() { if (p) (void)hipFreeAsync(p, st); }
+  ~AsyncBuf() { dev_release(p, st); }
 };
 
 // θ buffers the host-buffer pipeline rotates through: MCPX_HOST_BUFFERS (A/B knob, 2..8,
@@ -586,7 +638,7 @@ int solve_shard(int dev, const mcpx_desc* d, const double* theta, const double* 
   AsyncBuf<uint64_t> am;
   AsyncBuf<uint8_t> tr, fr;
   // declared after the buffers, so it runs before their (stream-ordered) frees on every
-  // exit: no upload or kernel may still target a buffer when it returns to the pool
+  // exit: no upload or kernel may still target a buffer when it returns to the cache
   struct Drain {
     hipStream_t a, b;
     ~Drain() {
@@ -759,7 +811,7 @@ int launch_sens_wg_impl(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, const Se
   const int64_t grid_max = std::min(slots_max, std::min(CH, d->batch));
   double* ws = nullptr;
   const size_t bytes = sizeof(double) * (size_t)(grid_max * w.slot_stride) + 256;
-  HIP_TRY(pool_malloc((void**)&ws, bytes, st));
+  HIP_TRY(dev_alloc((void**)&ws, bytes, st));
   w.work = ws;
   w.counter = (int32_t*)(ws + grid_max * w.slot_stride);
   int rc = MCPX_OK;
@@ -789,7 +841,7 @@ int launch_sens_wg_impl(bool jvp, const mcpx_desc* d, mcpx::SensArgs a, const Se
     }
     if (e != hipSuccess) rc = fail(MCPX_EHIP, "workgroup sensitivity launch failed: %s", hipGetErrorString(e));
   }
-  HIP_TRY(hipFreeAsync(ws, st));
+  dev_release(ws, st);
   return rc;
 }
 

@@ -9,10 +9,13 @@ oracle/ipm_oracle.c lu_band_solve).
   full-system LU (src/solver.jl:81-83) on every solved C4 game, with the divergences on the
   failing games recorded exactly.
 * GPU: mcpx_nl_solve_band bit-exact against the oracle's lu_band_solve mode on the C4 batch
-  with edge games, at the reference benchmark's horizon T = 10, and with warm starts.
+  with edge games, at the reference benchmark's horizon T = 10, with warm starts, and over
+  back-to-back host-buffer calls on both HIP runtimes (torch's and /opt/rocm's).
 """
 
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import pytest
@@ -20,6 +23,7 @@ import pytest
 from mcp_amd import _abi, band
 
 TRACE = 1024
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _z(r):
@@ -175,6 +179,40 @@ def test_gpu_band_t10(gpu, oracle_lib, B, warm):
     assert_parity(got, ref)
     if not warm:  # the bench's θ from x₀ = 0 (the zero-input warm start solves fewer: parity only)
         assert (ref["status"] == 0).mean() > 0.8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("runtime", ["torch", "system"])
+def test_gpu_host_calls_repeat_bit_exact(gpu, oracle_lib, runtime):
+    """Back-to-back host-buffer calls in one process (T = 10, 1,024 games): every call bit-exact
+    against the oracle.  "torch": this process (torch's bundled HIP runtime), two θ batches in
+    turn.  "system": a child process that never imports torch, so libmcpx.so runs on
+    /opt/rocm's HIP runtime — where the stream-ordered pool the library used to allocate from
+    (hipMallocFromPoolAsync, VM heap) returned wrong games from the fourth call on, every other
+    call (tools/band_stress.py); the library's block cache replaced it."""
+    if runtime == "system":
+        import json
+        import subprocess
+        import sys
+
+        env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
+        p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "band_stress.py"), "10", "1024", "band",
+                            "6", "reuse"], capture_output=True, text=True, timeout=150, env=env, cwd=ROOT)
+        assert p.returncode == 0, p.stderr[-2000:]
+        calls = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+        assert len(calls) == 6 and all(c["vs_oracle"] == 0 for c in calls), calls
+        return
+    from mcp_amd.batch import solve_batch
+    from tests.test_gpu_parity import assert_parity
+
+    game, tp = _c4(10, 2048)
+    mcp = game.mcp
+    batches = [np.ascontiguousarray(tp[:1024]), np.ascontiguousarray(tp[1024:])]
+    refs = [oracle_lib.solve_batch_nl(mcp.nl, t, linear_solver="schur", trace_len=TRACE, nthreads=8) for t in batches]
+    for call in range(6):
+        got = solve_batch(_abi.FAMILY_NONLINEAR, mcp.nl.n, mcp.nl.m, batches[call % 2], linear_solver="schur",
+                          trace_len=TRACE, module=mcp.module())
+        assert_parity(got, refs[call % 2])
 
 
 @pytest.mark.gpu
