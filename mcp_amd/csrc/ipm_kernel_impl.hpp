@@ -499,6 +499,36 @@ __device__ __forceinline__ double dot_strided(const double* __restrict__ p, int 
   return acc;
 }
 
+#ifndef MCPX_RES_INC
+#define MCPX_RES_INC 1
+#endif
+// dot_strided (NEG = false) with the addresses formed by a running pointer, one 64-bit add
+// per element (the empty asm keeps the compiler from re-deriving p + j·st with a multiply).
+// The residual's M·x | A·x reads a lane-dependent pointer and stride (M column in θ, A row
+// in LDS); from p + j·st the compiler spent a multiply, a shift and a 64-bit add on each
+// element (≈ 96 VALU a Newton step at C3), here one add (MCPX_RES_INC; same loads, same
+// bits; C3 8,192: 12.56 against 12.21 M solves/s, profiles/r05/ab_res_inc.jsonl).
+template <int BATCH>
+__device__ __forceinline__ double dot_strided_inc(const double* __restrict__ p, int st, const double* q, int cnt,
+                                                  double acc) {
+  const int64_t sb = (int64_t)st * 8;
+  const char* pc = (const char*)p;
+  for (int j0 = 0; j0 < cnt; j0 += BATCH) {
+    double t[BATCH];
+#pragma unroll
+    for (int b = 0; b < BATCH; ++b) {
+      t[b] = *(const double*)pc;
+      if (j0 + b + 1 < cnt) pc += sb;  // the last element repeats (clamped, always valid)
+      asm volatile("" : "+v"(pc));
+    }
+#pragma unroll
+    for (int b = 0; b < BATCH; ++b)
+      if (j0 + b < cnt) acc = fma(t[b], q[j0 + b], acc);
+    __builtin_amdgcn_sched_barrier(0);  // at most BATCH loads in flight (register budget)
+  }
+  return acc;
+}
+
 // SCHUR path (QP family, and the affine family with ∂H/∂y ≡ 0), part 1: residuals.
 // x-lanes compute F_G, y-lanes (which also own s_k) F_H and F_C; same fma order as
 // family_row() of the oracle.  `ta` is the H-side coupling (QP: A; affine: R) with
@@ -514,7 +544,8 @@ __device__ __forceinline__ void qp_residuals(const double* __restrict__ th, cons
   const int kh = ln - n;
   const double* px = rg ? th + ln : (rh ? ta + kh : th);  // M column (θ) | A row
   const int sx = rg ? n : (rh ? lda : 0);
-  double acc = dot_strided<BATCH, false>(px, sx, zs, n, 0.0);  // M_ij x_j  |  A_kj x_j
+  double acc = MCPX_RES_INC ? dot_strided_inc<BATCH>(px, sx, zs, n, 0.0)   // M_ij x_j  |  A_kj x_j
+                            : dot_strided<BATCH, false>(px, sx, zs, n, 0.0);
   const double acc_y = dot_strided<BATCH, true>(tq + (rg ? ln * ldq : 0), 1, zs + n, m, acc);  // − A_ki y_k
   if (rg) acc = acc_y;
   F = 0.0;
