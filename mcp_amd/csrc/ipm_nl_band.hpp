@@ -139,6 +139,14 @@ __device__ __forceinline__ int pivot_exact(const double (&col)[NJ], const int (&
   return ps;
 }
 
+// MCPX_BAND_TWICE (diagnostic builds only, tools/band_ab.py): one phase of the Newton step
+// runs twice — 1 factorisation and back substitution, 2 formation of S' and rr', 3 the
+// generated eval, 4 back substitution.  Each phase is idempotent, so the bits stay the
+// product's and the time added is the phase's cost.
+#ifndef MCPX_BAND_TWICE
+#define MCPX_BAND_TWICE 0
+#endif
+
 constexpr int US = WC + 2;   // U row stride: the WC window entries, the rhs, 1 / u_kk
 constexpr int EMAX = MCPX_NL_BAND_EMAX;  // nonzeros per S' row (the entering-row table's width)
 constexpr bool ULDS = (int64_t)n * US * 8 <= 8 * 1024;
@@ -269,6 +277,7 @@ __device__ __forceinline__ bool factor_solve(const double* Sc, const double* rrp
     });
   }
   if (fail) return false;
+  for (int rep = 0; rep < (MCPX_BAND_TWICE == 4 ? 2 : 1); ++rep) {
   // ---- back substitution, k = n − 1 .. 0 (lane l: the rhs and 1 / u_tt of row t ≡ l mod 64,
   // the largest such t ≤ k; rows enter the update window [k − WC + 1, k − 1] WC − 1 steps
   // before their x) --------------------------------------------------------------------------
@@ -315,6 +324,7 @@ __device__ __forceinline__ bool factor_solve(const double* Sc, const double* rrp
         }
       }
     });
+  }
   }
   return true;
 }
@@ -417,7 +427,7 @@ __device__ __forceinline__ void solve(const wg::WgArgs& A) {
         const int ln = opaque_lane(ln0);
         __syncthreads();
 #if defined(MCPX_NL_CVEC)
-        eval_cvec(ev, vw, vd);
+        for (int rep = 0; rep < (MCPX_BAND_TWICE == 3 ? 2 : 1); ++rep) eval_cvec(ev, vw, vd);
 #else
         if (ln == 0) mcpx_nl_eval_c(th, zs, cb);
 #endif
@@ -451,6 +461,7 @@ __device__ __forceinline__ void solve(const wg::WgArgs& A) {
         __syncthreads();
         // S' entries and rr' (oracle: the row-wise loops over K(i) and J(k), the same chains);
         // rounds one at a time (unrolled, all their table loads would be in flight at once)
+        for (int rep = 0; rep < (MCPX_BAND_TWICE == 2 ? 2 : 1); ++rep) {
 #pragma unroll 1
         for (int r = 0; r < MCPX_NL_BF_R; ++r) {
           constexpr int WD = 1 + 2 * MCPX_NL_BF_KT;
@@ -484,8 +495,10 @@ __device__ __forceinline__ void solve(const wg::WgArgs& A) {
             rrp[i] = v;
           }
         }
+        }
         __syncthreads();
-        const bool ok = factor_solve(Sc, rrp, dxp, img2, U, ent_tab, ln);
+        bool ok = factor_solve(Sc, rrp, dxp, img2, U, ent_tab, ln);
+        if (MCPX_BAND_TWICE == 1) ok = factor_solve(Sc, rrp, dxp, img2, U, ent_tab, ln);
         if (!ok) {  // the failed linear solve of :84-88
           status = 1;
           reason |= MCPX_FAIL_LINSOLVE;
