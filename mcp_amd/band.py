@@ -256,9 +256,11 @@ class BandPlan:
     def lds_bytes(self, ev_size: int) -> int:
         """Static LDS of mcpx_nl_solve_band (the static_assert of csrc/ipm_nl_band.hpp): ev, S'
         values + a zero, rr', D⁻¹ and ty, δx (S' order), two entering-row images, and the U rows
-        (WC + 2 doubles each) when they take at most 8 KB (else the slot's HBM workspace)."""
+        (WC + 2 doubles each) when they take at most 8 KB (else the slot's HBM workspace, and each
+        row's rhs and 1 / u_kk in LDS for the back substitution: 2n doubles)."""
         u = self.n * (self.wc + 2)
-        return 8 * (ev_size + self.nnz_s + 1 + self.n + 2 * self.m + self.n + 2 * self.wc + (u if 8 * u <= 8 * 1024 else 0))
+        lds_u = u if 8 * u <= 8 * 1024 else 2 * self.n
+        return 8 * (ev_size + self.nnz_s + 1 + self.n + 2 * self.m + self.n + 2 * self.wc + lds_u)
 
 
 def plan(nl) -> BandPlan | None:

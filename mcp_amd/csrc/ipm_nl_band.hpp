@@ -54,9 +54,7 @@ constexpr int kCVecSteps[] = {MCPX_NL_CVEC_STEPS};
 constexpr int EVN = CS + N, OFFZ = CS;
 #endif
 // the LDS codegen.py budgets for (NLSystem._emit_band: band.BandPlan.lds_bytes)
-static_assert(8 * (EVN + NNZ + 1 + n + 2 * m + n + 2 * WC + ((int64_t)n * (WC + 2) * 8 <= 8 * 1024 ? n * (WC + 2) : 0)) <=
-                  40 * 1024,
-              "band kernel LDS");
+
 
 __device__ __forceinline__ const int* opaque_ptr(const int* p) {
   asm volatile("" : "+s"(p));
@@ -143,6 +141,9 @@ __device__ __forceinline__ int pivot_exact(const double (&col)[NJ], const int (&
 // runs twice — 1 factorisation and back substitution, 2 formation of S' and rr', 3 the
 // generated eval, 4 back substitution.  Each phase is idempotent, so the bits stay the
 // product's and the time added is the phase's cost.
+#ifndef MCPX_BAND_BS_NOBR
+#define MCPX_BAND_BS_NOBR 1
+#endif
 #ifndef MCPX_BAND_TWICE
 #define MCPX_BAND_TWICE 0
 #endif
@@ -155,6 +156,12 @@ constexpr int UD = ULDS ? 4 : WC;  // back-substitution prefetch distance (divid
 // prefetch of rows that are read and discarded
 constexpr int64_t WS = ULDS ? 0 : (int64_t)(n + 64) * US;
 static_assert(WC % UD == 0 && EMAX <= 64, "band tables");
+// MCPX_BAND_BS_NOBR with the U rows in HBM: each row's rhs and 1 / u_kk also go to LDS (sBR,
+// 2n doubles), so the back substitution's entering rows come from LDS, not from branch-guarded
+// loads (see factor_solve).
+constexpr bool BSL = !ULDS && MCPX_BAND_BS_NOBR;
+static_assert(8 * (EVN + NNZ + 1 + n + 2 * m + n + 2 * WC + (ULDS ? n * US : 0) + (BSL ? 2 * n : 0)) <= 40 * 1024,
+              "band kernel LDS (mcp_amd/band.py BandPlan.lds_bytes)");
 
 struct Win {
   double acc[NJ][NCB], rh[NJ];
@@ -186,7 +193,7 @@ __device__ __forceinline__ void enter(Win& w, int R, int ls, const double* img, 
 // Elimination step k (lu_band_solve's step k), W = k mod WC static.  `fail`: a zero pivot.
 template <int W>
 __device__ __forceinline__ void step(Win& w, int k, const double* Sc, const double* rrp, double* img2,
-                                     double* U, const int* ent_tab, int& ent, int ln, bool& fail) {
+                                     double* U, double* sBR, const int* ent_tab, int& ent, int ln, bool& fail) {
   constexpr int CK = W >> 2, QK = W & 3;
   const int lc = ln & 15, lr = ln >> 4;
   double col[NJ];
@@ -223,8 +230,13 @@ __device__ __forceinline__ void step(Win& w, int k, const double* Sc, const doub
     for (int c = 0; c < NCB; ++c) Uk[4 * c + lr] = u[c];
   }
   if (ln == 0) {
-    Uk[WC] = ub;
-    Uk[WC + 1] = rp;
+    if constexpr (BSL) {
+      sBR[2 * k] = ub;
+      sBR[2 * k + 1] = rp;
+    } else {
+      Uk[WC] = ub;
+      Uk[WC + 1] = rp;
+    }
   }
 #pragma unroll
   for (int J = 0; J < NJ; ++J) {
@@ -248,7 +260,7 @@ __device__ __forceinline__ void step(Win& w, int k, const double* Sc, const doub
 // lu_band_solve on S' (Sc: the entries in S' row-major order, ent_tab: each row's (window index,
 // entry) pairs) and rr' (rrp, S' row order): x' (S' column order) into dxp.  False: a zero pivot.
 __device__ __forceinline__ bool factor_solve(const double* Sc, const double* rrp, double* dxp, double* img2,
-                                             double* U, const int* ent_tab, int ln) {
+                                             double* U, double* sBR, const int* ent_tab, int ln) {
   const int lc = ln & 15, lr = ln >> 4;
   Win w;
 #pragma unroll
@@ -272,8 +284,8 @@ __device__ __forceinline__ bool factor_solve(const double* Sc, const double* rrp
 #pragma unroll 1
   for (int k0 = 0; k0 < n; k0 += WC) {
     static_for<0, WC>([&](auto W) {
-      if (k0 + decltype(W)::value < n) step<decltype(W)::value>(w, k0 + decltype(W)::value, Sc, rrp, img2, U, ent_tab,
-                                                                ent, ln, fail);
+      if (k0 + decltype(W)::value < n) step<decltype(W)::value>(w, k0 + decltype(W)::value, Sc, rrp, img2, U, sBR,
+                                                                ent_tab, ent, ln, fail);
     });
   }
   if (fail) return false;
@@ -283,42 +295,67 @@ __device__ __forceinline__ bool factor_solve(const double* Sc, const double* rrp
   // before their x) --------------------------------------------------------------------------
   if constexpr (!ULDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the U rows are stored
   __syncthreads();
-  const int top = n - 1;
+  constexpr int top = n - 1;
   int t = top - ((top - ln) & 63);  // this lane's row
   double bs = 0.0, rd = 0.0, nb = 0.0, nr = 0.0;
   if (t >= 0) {
-    bs = U[(int64_t)t * US + WC];
-    rd = U[(int64_t)t * US + WC + 1];
+    bs = BSL ? sBR[2 * t] : U[(int64_t)t * US + WC];
+    rd = BSL ? sBR[2 * t + 1] : U[(int64_t)t * US + WC + 1];
+  }
+  // BSL: the pair (rhs, 1 / u) of the row entering at the next step, read from LDS a step ahead
+  double pb = 0.0, pc = 0.0;
+  if constexpr (BSL) {
+    const int i = top - WC + 1 > 0 ? top - WC + 1 : 0;
+    pb = sBR[2 * i];
+    pc = sBR[2 * i + 1];
   }
   double ring[UD];
+  // MCPX_BAND_BS_NOBR: the back substitution's loads are issued by every lane from a valid
+  // (clamped) address and selected afterwards.  Behind a branch, a load the compiler cannot
+  // count through made it wait vmcnt(0) at every step — for the prefetches issued UD steps
+  // ahead too, a memory round trip per step.
   auto prefetch = [&](int kk) {  // U_{t(kk), kk} of step kk into ring[kk mod UD] (rows outside the window: discarded)
     const int tt = kk - ((kk - ln) & 63);
+    if constexpr (MCPX_BAND_BS_NOBR) {  // raw: a lane without a row (tt < 0) never feeds an x
+      const bool ok = tt >= 0 && kk >= 0;
+      return U[(int64_t)(ok ? tt : 0) * US + (kk >= 0 ? kk % WC : 0)];
+    }
     return tt >= 0 && kk >= 0 ? U[(int64_t)tt * US + kk % WC] : 0.0;
   };
-  const int kb = top - top % WC;  // the block of k = top (k mod WC static inside a block)
 #pragma unroll
   for (int d = 0; d < UD; ++d) ring[(top - d) % UD] = prefetch(top - d);
+  // k = top, top − 1, …, in blocks of WC steps (k mod WC static in a block); the last block's
+  // steps past k = 0 run as no-ops (no row takes part, no x is stored) instead of behind a
+  // branch: a branch around the prefetches would again cost a vmcnt(0) at every step
 #pragma unroll 1
-  for (int b0 = kb; b0 >= 0; b0 -= WC) {
+  for (int s0 = 0; s0 < n; s0 += WC) {
     static_for<0, WC>([&](auto JJ) {
-      constexpr int W = WC - 1 - decltype(JJ)::value;  // k mod WC
-      const int k = b0 + W;
-      if (k <= top) {
+      constexpr int W = ((top - decltype(JJ)::value) % WC + WC) % WC;  // k mod WC
+      const int k = top - s0 - decltype(JJ)::value;
+      {
         // row k − WC + 1 enters the update window: its lane (done with row k − WC + 65) takes its
         // rhs and 1 / u, loaded when that row finished (WC − 1 steps before the lane row's x)
         const int ta = k - WC + 1;
-        if (ta >= 0 && ta + 64 <= top && (ta & 63) == ln) {
+        if constexpr (BSL) {
+          const bool tk = ta >= 0 && ta + 64 <= top && (ta & 63) == ln;
+          bs = tk ? pb : bs;
+          rd = tk ? pc : rd;
+        } else if (ta >= 0 && ta + 64 <= top && (ta & 63) == ln) {
           bs = nb;
           rd = nr;
         }
         const double xk = bcast(bs * rd, k & 63);
-        if (ln == 0) dxp[k] = xk;
+        if (ln == 0 && k >= 0) dxp[k] = xk;
         const int tl = k - ((k - ln) & 63);  // this lane's row at step k
         const double uv = ring[W % UD];
         const double nbs = fma(-uv, xk, bs);
         bs = (tl >= k - WC + 1 && tl <= k - 1) ? nbs : bs;
         ring[W % UD] = prefetch(k - UD);
-        if ((k & 63) == ln && k >= 64) {  // row k is done: its lane's next row is k − 64
+        if constexpr (BSL) {  // the next step's entering row
+          const int i = ta - 1 > 0 ? ta - 1 : 0;
+          pb = sBR[2 * i];
+          pc = sBR[2 * i + 1];
+        } else if ((k & 63) == ln && k >= 64) {  // row k is done: its lane's next row is k − 64
           nb = U[(int64_t)(k - 64) * US + WC];
           nr = U[(int64_t)(k - 64) * US + WC + 1];
         }
@@ -365,6 +402,7 @@ __device__ __forceinline__ void solve(const wg::WgArgs& A) {
   __shared__ __attribute__((aligned(16))) double ev[EVN];
   __shared__ double Sc[NNZ + 1], rrp[n], sDi[imax(1, m)], sTy[imax(1, m)], dxp[n], img2[2 * WC];
   __shared__ double Ush[ULDS ? n * US : 1];
+  __shared__ double sBR[BSL ? 2 * n : 1];
   double* const cb = ev;
   double* const zs = ev + OFFZ;
   const int ln0 = threadIdx.x;
@@ -497,8 +535,8 @@ __device__ __forceinline__ void solve(const wg::WgArgs& A) {
         }
         }
         __syncthreads();
-        bool ok = factor_solve(Sc, rrp, dxp, img2, U, ent_tab, ln);
-        if (MCPX_BAND_TWICE == 1) ok = factor_solve(Sc, rrp, dxp, img2, U, ent_tab, ln);
+        bool ok = factor_solve(Sc, rrp, dxp, img2, U, sBR, ent_tab, ln);
+        if (MCPX_BAND_TWICE == 1) ok = factor_solve(Sc, rrp, dxp, img2, U, sBR, ent_tab, ln);
         if (!ok) {  // the failed linear solve of :84-88
           status = 1;
           reason |= MCPX_FAIL_LINSOLVE;
