@@ -57,7 +57,7 @@ extern "C" {
  * struct's size and layout: a caller built against a 1.x header passes a shorter
  * struct, so the major version moved.  Callers check mcpx_version() / 10000 against
  * MCPX_VERSION / 10000 before the first call (mcp_amd/_lib.py does). */
-#define MCPX_VERSION 20100 /* 2.1.0: mcpx_cond_batch* */
+#define MCPX_VERSION 20200 /* 2.1.0: mcpx_cond_batch*; 2.2.0: MCPX_FAIL_INPUT */
 
 /* error codes */
 #define MCPX_OK 0
@@ -74,6 +74,10 @@ extern "C" {
 #define MCPX_FAIL_LINSOLVE 1u   /* a Newton system was singular, a zero pivot (:84-88) */
 #define MCPX_FAIL_LINESEARCH 2u /* the fraction-to-the-boundary line search gave NaN (:93-99) */
 #define MCPX_FAIL_MAX_OUTER 4u  /* outer_iters reached max_outer_iters (:117-119) */
+/* the instance is outside what the chosen elimination is exact for, so it was not solved:
+ * MCPX_LINSOLVE_SCHUR on an affine θ whose S block (∂H/∂y) is not exactly zero.  The record
+ * is status FAILED, kkt_error NaN, the initial point, outer_iters 1, newton_iters 0. */
+#define MCPX_FAIL_INPUT 8u
 
 #define MCPX_FAMILY_QP 0
 #define MCPX_FAMILY_AFFINE 1
@@ -121,8 +125,9 @@ extern "C" {
  *                         Schur complement (default; N ≤ 64 means n + m ≤ 64);
  *  MCPX_LINSOLVE_DENSE    dense LU with partial pivoting of the full
  *                         (n+2m)-dim system (n + 2m ≤ 64);
- *  MCPX_LINSOLVE_SCHUR    ∂H/∂y = 0 (QP family; affine family, whose S block is
- *                         then NOT read — ∂H/∂y is taken as 0; generated modules
+ *  MCPX_LINSOLVE_SCHUR    ∂H/∂y = 0 (QP family; affine family, whose S block must
+ *                         then be exactly 0 — an instance with any nonzero (or NaN)
+ *                         S entry is not solved and reports MCPX_FAIL_INPUT; generated modules
  *                         without an ∂H/∂y block): after the slack block, the
  *                         now-diagonal y block is eliminated as well, leaving the
  *                         n×n Schur complement S = (M + tol·I) + Aᵀ D⁻¹ A (affine:

@@ -14,6 +14,7 @@ STATUS_FAILED = 1
 FAIL_LINSOLVE = 1
 FAIL_LINESEARCH = 2
 FAIL_MAX_OUTER = 4
+FAIL_INPUT = 8  # SCHUR on an affine θ with a nonzero S block: not solved
 
 FAMILY_QP = 0
 FAMILY_AFFINE = 1

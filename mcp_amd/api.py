@@ -545,9 +545,12 @@ def _linear_solver(mcp: PrimalDualMCP, linear_solve_algorithm) -> str:
     if linear_solve_algorithm is None:
         if mcp.family == _abi.FAMILY_NONLINEAR:
             return mcp.nl.default_solver()
-        # the MFMA Schur-complement kernel wherever it applies (∂H/∂y ≡ 0, one wave: n + m ≤ 64)
+        # the MFMA Schur-complement kernel for the QP family (one wave: n + m ≤ 64).  An
+        # affine-family MCP here has −Q ≠ Rᵀ symbolically (else it is classified QP), so its
+        # SCHUR solve would always take the pivoting-LU pass, whose rate is not the measured
+        # one: REDUCED (pivoting over the whole n + m system) stays its default.
         one_wave = mcp.unconstrained_dimension + mcp.constrained_dimension <= _abi.MAX_KKT_DIM
-        return "schur" if mcp.h_independent_of_y and one_wave else "reduced"
+        return "schur" if mcp.family == _abi.FAMILY_QP and one_wave else "reduced"
     if isinstance(linear_solve_algorithm, str):
         if linear_solve_algorithm not in _abi.LINEAR_SOLVERS:
             raise ValueError(f"linear_solve_algorithm must be one of {sorted(_abi.LINEAR_SOLVERS)}")

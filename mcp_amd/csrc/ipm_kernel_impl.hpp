@@ -1252,8 +1252,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   // SCHUR: M exactly symmetric ⇒ S symmetric ⇒ try the pivot-free SPD
   // Gauss-Jordan first (oracle: m_sym).  Once per instance.
   bool spd_try = false;
+  bool s_bad = false;  // affine SCHUR: an S entry ≠ 0 (or NaN) — not solved, MCPX_FAIL_INPUT
   if constexpr (SCH) {
     const int n = n0;
+    if constexpr (AFF) {
+      const int m = m0;
+      const double* ts = th0 + n * n + 2 * n * m;
+      bool nz = false;
+      for (int i = lane; i < m * m; i += 64) nz |= !(ts[i] == 0.0);
+      s_bad = ballot(nz) != 0ull;
+    }
     bool asym = false;
     const int r = min(lane, max(n - 1, 0));
 #pragma clang loop unroll(disable)
@@ -1275,7 +1283,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
         asym |= !(sQ[r * (m + 1) + k] == th0[n * n + n * m + i]);
       }
     }
-    spd_try = ballot(asym) == 0ull;
+    spd_try = ballot(asym) == 0ull || s_bad;  // (s_bad: no Newton step is taken)
     if constexpr (PASS == 1) {
       if (!spd_try) {  // needs the pivoting LU at every step: second pass
         if (lane == 0) args.status[inst] = STATUS_DEFERRED;
@@ -1290,6 +1298,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PASS == 1 ? 
   int outer = 1;                       // :70
   int newton = 0;
   unsigned reason = 0;  // MCPX_FAIL_* events
+  if (s_bad) {  // the while condition is false on a NaN kkt: the initial point is returned
+    kkt = __builtin_nan("");
+    status = MCPX_STATUS_FAILED;
+    reason = MCPX_FAIL_INPUT;
+  }
 #if MCPX_STAMPS == 1
   uint64_t st_acc[MCPX_NSTAMP] = {};
   uint64_t st_last = __builtin_amdgcn_s_memtime();

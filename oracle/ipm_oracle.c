@@ -482,6 +482,18 @@ static void solve_one(const mcpx_desc* d, const double* th, const double* x0, co
             break;
           }
   }
+  if (schur_dense && d->family == MCPX_FAMILY_AFFINE) {
+    /* SCHUR takes ∂H/∂y ≡ 0: an affine θ with an S entry ≠ 0 (or NaN) is not solved
+       (MCPX_FAIL_INPUT, include/mcpx.h) — the loop below does not run on a NaN kkt */
+    const double* S = th + (size_t)n * n + 2 * (size_t)n * m;
+    for (size_t i = 0; i < (size_t)m * m; ++i)
+      if (!(S[i] == 0.0)) {
+        kkt = NAN;
+        status = MCPX_STATUS_FAILED;
+        reason = MCPX_FAIL_INPUT;
+        break;
+      }
+  }
   while (kkt > p->tol && eps > p->tol && outer < p->max_outer_iters) { /* :71 */
     int inner = 1;            /* :72 */
     status = MCPX_STATUS_SOLVED; /* :73 */

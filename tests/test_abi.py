@@ -45,7 +45,7 @@ def test_library_has_gfx950_code_object():
 
 def test_version_and_constants():
     L = lib()
-    assert L.mcpx_version() == 20100
+    assert L.mcpx_version() == 20200
     for fam, (n, m) in [(0, (2, 2)), (0, (32, 16)), (1, (4, 8))]:
         assert L.mcpx_theta_dim(fam, n, m) == _abi.theta_dim(fam, n, m)
     assert L.mcpx_theta_dim(9, 2, 2) < 0 and L.mcpx_theta_dim(0, -1, 2) < 0

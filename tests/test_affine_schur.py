@@ -1,5 +1,5 @@
 """The SCHUR solve of the affine family (∂H/∂y ≡ 0): θ' = [P; Q; R; S; g; h] with the S block
-not read, S_ij = P_ij + Σ_k (−Q_ik)·(R_kj·D_k⁻¹) formed on the matrix cores (ipm_kernel_impl.hpp,
+exactly zero (an instance with a nonzero S entry is not solved: MCPX_FAIL_INPUT), S_ij = P_ij + Σ_k (−Q_ik)·(R_kj·D_k⁻¹) formed on the matrix cores (ipm_kernel_impl.hpp,
 AFF), the same kernel as the QP family's with R in A's place and −Qᵀ, −h, −g in LDS.
 
 This is the path a reference user's MCP takes through the C ABI: the Julia shim
@@ -9,8 +9,9 @@ arrives as P = M, Q = −Aᵀ, R = A, S = 0, g = −ϕ, h = −b.
 
 * CPU: that embedding is bit-identical to the QP family's SCHUR solve in the oracle (every
   field); a perturbed, non-symmetric coupling (−Q ≠ Rᵀ: the pivoting-LU pass) agrees with the
-  REDUCED elimination on solved instances; the S block is ignored; the Python API picks SCHUR
-  exactly when S ≡ 0 symbolically.
+  REDUCED elimination on solved instances; a nonzero or NaN S entry gives the MCPX_FAIL_INPUT
+  record; the Python API defaults to REDUCED for the affine family (its SCHUR instances never
+  take the SPD pass: the QP-shaped ones are classified QP) and accepts SCHUR when S ≡ 0.
 * GPU: bit-exact against the oracle at C3's shape (the compile-time kernel) and the runtime
   buckets, symmetric and not, with NaN / Inf / huge inputs; and equal to the QP kernel's bits
   on the embedding.
@@ -31,7 +32,7 @@ FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_it
 
 
 def qp_to_affine(th: np.ndarray, n: int, m: int, s_fill: float = 0.0) -> np.ndarray:
-    """mcp_amd.qp_benchmark.affine_embedding, with the (unread) S block filled with `s_fill`."""
+    """mcp_amd.qp_benchmark.affine_embedding, with the S block filled with `s_fill`."""
     out = affine_embedding(th, n, m)
     out[:, n * n + 2 * n * m:n * n + 2 * n * m + m * m] = s_fill
     return out
@@ -59,14 +60,36 @@ def test_oracle_qp_embedding_is_bit_identical(oracle_lib, n, m, sp):
         assert _same(q[f], a[f]), f
 
 
-def test_oracle_s_block_is_not_read(oracle_lib):
+def test_oracle_nonzero_s_block_is_rejected(oracle_lib):
+    """SCHUR eliminates y through the diagonal D, exact only for ∂H/∂y ≡ 0: an instance whose
+    S block holds any nonzero or NaN entry returns the MCPX_FAIL_INPUT record (status failed,
+    kkt NaN, the initial point, outer 1, no Newton step); S = −0.0 is zero."""
     n, m = 8, 4
     th = generate_random_parameter(np.random.default_rng(7), n, m, 0.0, batch=32)
     a = oracle_lib.solve_batch(AFF, n, m, qp_to_affine(th, n, m), linear_solver="schur", trace_len=TRACE)
-    b = oracle_lib.solve_batch(AFF, n, m, qp_to_affine(th, n, m, s_fill=np.nan), linear_solver="schur",
+    z = oracle_lib.solve_batch(AFF, n, m, qp_to_affine(th, n, m, s_fill=-0.0), linear_solver="schur",
                                trace_len=TRACE)
     for f in FIELDS:
-        assert _same(a[f], b[f]), f
+        assert _same(a[f], z[f]), f
+    th_bad = qp_to_affine(th, n, m)
+    s0 = n * n + 2 * n * m
+    th_bad[0, s0] = np.nan
+    th_bad[1, s0 + m * m - 1] = 1e-300
+    th_bad[2, s0:s0 + m * m] = 7.0
+    b = oracle_lib.solve_batch(AFF, n, m, th_bad, linear_solver="schur", trace_len=TRACE)
+    assert (a["status"][:3] == 0).all()
+    np.testing.assert_array_equal(b["status"][:3], 1)
+    np.testing.assert_array_equal(b["fail_reason"][:3], _abi.FAIL_INPUT)
+    assert np.isnan(b["kkt_error"][:3]).all()
+    np.testing.assert_array_equal(b["outer_iters"][:3], 1)
+    np.testing.assert_array_equal(b["newton_iters"][:3], 0)
+    np.testing.assert_array_equal(b["x"][:3], 0.0)
+    np.testing.assert_array_equal(b["y"][:3], 1.0)
+    for f in FIELDS:  # the other instances are untouched
+        assert _same(a[f][3:], b[f][3:]), f
+    # REDUCED reads S: the same θ solves there
+    r = oracle_lib.solve_batch(AFF, n, m, th_bad[1:3], linear_solver="reduced")
+    assert (r["fail_reason"] & _abi.FAIL_INPUT == 0).all()
 
 
 @pytest.mark.parametrize("n,m", [(32, 16), (12, 8)])
@@ -101,12 +124,16 @@ def _sym_mcp(S_zero: bool):
     return PrimalDualMCP(G, H, unconstrained_dimension=2, constrained_dimension=2, parameter_dimension=3)
 
 
-def test_api_picks_schur_when_h_does_not_depend_on_y():
+def test_api_affine_defaults_to_reduced_and_accepts_schur_when_h_does_not_depend_on_y():
+    """An affine-family MCP from the front end has −Q ≠ Rᵀ symbolically (else it is classified
+    QP), so SCHUR would always run its pivoting-LU pass: the default stays REDUCED, and SCHUR is
+    accepted on request when ∂H/∂y ≡ 0."""
     from mcp_amd.api import InteriorPoint, _linear_solver, solve
 
     mcp = _sym_mcp(True)
     assert mcp.family == AFF and mcp.h_independent_of_y
-    assert _linear_solver(mcp, None) == "schur"
+    assert _linear_solver(mcp, None) == "reduced"
+    assert _linear_solver(mcp, "schur") == "schur"
     mcp_s = _sym_mcp(False)
     assert mcp_s.family == AFF and not mcp_s.h_independent_of_y
     assert _linear_solver(mcp_s, None) == "reduced"
@@ -149,21 +176,24 @@ def test_gpu_affine_schur_edge_inputs(gpu, oracle_lib):
     th[2, :] = 0.0
     th[3, n * n + n * m + 5] = 1e200  # R
     th[4, -1] = -np.inf  # h
-    th[5, n * n + 2 * n * m:n * n + 2 * n * m + m * m] = 7.0  # S: not read
+    th[5, n * n + 2 * n * m:n * n + 2 * n * m + m * m] = 7.0  # S ≠ 0: MCPX_FAIL_INPUT
+    th[7, n * n + 2 * n * m + 3] = np.nan  # likewise
     th[6, -m - 1] = 1e-300  # g
     got = solve_batch(AFF, n, m, th, linear_solver="schur", trace_len=TRACE)
     ref = oracle_lib.solve_batch(AFF, n, m, th, linear_solver="schur", trace_len=TRACE)
     assert_parity(got, ref)
+    np.testing.assert_array_equal(got["fail_reason"][[5, 7]], _abi.FAIL_INPUT)
+    assert (got["fail_reason"][[1, 2, 3, 4, 6]] & _abi.FAIL_INPUT == 0).all()
 
 
 @pytest.mark.gpu
 def test_gpu_api_game_takes_affine_schur(gpu, oracle_lib):
-    """solve() on an affine MCP with ∂H/∂y ≡ 0 runs SCHUR (its default) with the oracle's bits."""
+    """solve() on an affine MCP with ∂H/∂y ≡ 0 runs SCHUR on request with the oracle's bits."""
     from mcp_amd.api import InteriorPoint, solve
 
     mcp = _sym_mcp(True)
     th = np.random.default_rng(2).standard_normal((64, 3))
-    sol = solve(InteriorPoint(), mcp, th, tol=1e-6)
+    sol = solve(InteriorPoint(), mcp, th, tol=1e-6, linear_solve_algorithm="schur")
     ref = oracle_lib.solve_batch(AFF, 2, 2, mcp.theta_map(th), tol=1e-6, linear_solver="schur")
     np.testing.assert_array_equal(sol.x, ref["x"])
     np.testing.assert_array_equal(sol.y, ref["y"])
