@@ -63,13 +63,14 @@ def window(S: np.ndarray, cperm, rperm=None) -> tuple[int, int]:
     LU), so WC − 1 ≥ that − k."""
     n = S.shape[0]
     Sc = S[:, cperm]
-    f = np.array([np.nonzero(Sc[r])[0].min() for r in range(n)])
-    l = np.array([np.nonzero(Sc[r])[0].max() for r in range(n)])
+    f = Sc.argmax(1)                      # first nonzero column (every row has its diagonal)
+    l = n - 1 - Sc[:, ::-1].argmax(1)     # last nonzero column
     rp = np.lexsort((np.arange(n), f)) if rperm is None else np.asarray(rperm)
     fs, ls = f[rp], l[rp]
-    W = int(max(i + 1 - fs[i] for i in range(n)))
+    k = np.arange(n)
+    W = int((k + 1 - fs).max())
     lmax = np.maximum.accumulate(ls)
-    Wc = int(max(lmax[min(n, k + W) - 1] - k + 1 for k in range(n)))
+    Wc = int((lmax[np.minimum(n, k + W) - 1] - k + 1).max())
     return W, Wc
 
 
@@ -78,6 +79,10 @@ def row_order(S: np.ndarray, cperm) -> np.ndarray:
     n = S.shape[0]
     f = np.array([np.nonzero(S[r][cperm])[0].min() for r in range(n)])
     return np.lexsort((np.arange(n), f)).astype(np.int64)
+
+
+CM_EXHAUSTIVE = 1024
+CM_STARTS = 16
 
 
 def cm_order(S: np.ndarray) -> np.ndarray:
@@ -109,7 +114,10 @@ def cm_order(S: np.ndarray) -> np.ndarray:
     head = []
     for ci, comp in enumerate(big):
         best = None
-        for s in comp:
+        # every start vertex up to CM_EXHAUSTIVE vertices (each trial is an O(n²) window);
+        # beyond that the CM_STARTS lowest-degree vertices (the pseudo-peripheral candidates)
+        starts = comp if len(comp) <= CM_EXHAUSTIVE else sorted(comp, key=lambda v: (deg[v], v))[:CM_STARTS]
+        for s in starts:
             o, mark, q = [s], {s}, 0
             while q < len(o):
                 v = o[q]

@@ -150,9 +150,8 @@ def alloc_device_outputs(B: int, n: int, m: int, device, trace_len: int = 0, new
         kkt_error=torch.empty(B, **f64), eps=torch.empty(B, **f64),
         outer_iters=torch.empty(B, **i32), status=torch.empty(B, **i32),
         newton_iters=torch.empty(B, **i32) if newton else None,
-        # one uint64 word per instance up to m = 64 (shape (B,)), else (B, ⌈m/64⌉) words
-        active_mask=(torch.empty(B, dtype=torch.int64, device=device) if m <= 64 else
-                     torch.empty(B, (m + 63) // 64, dtype=torch.int64, device=device)) if active else None,
+        # (B, W) uint64 words, W = max(1, ⌈m/64⌉) — the host path's and distributed.py's shape
+        active_mask=torch.empty(B, max(1, (m + 63) // 64), dtype=torch.int64, device=device) if active else None,
         alpha_trace=torch.full((B, trace_len, 2), 254, dtype=torch.uint8, device=device) if trace_len > 0 else None,
         fail_reason=torch.empty(B, dtype=torch.uint8, device=device),
     )

@@ -223,6 +223,8 @@ def test_device_api_matches_host_api(gpu):
     torch.cuda.synchronize()
     for k in ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters"):
         np.testing.assert_array_equal(dev[k].cpu().numpy(), host[k], err_msg=k)
+    # the active set: (B, W) uint64 words on both paths (W = 1 here)
+    np.testing.assert_array_equal(dev["active_mask"].cpu().numpy().view(np.uint64), host["active_mask"])
 
 
 @pytest.mark.parametrize("ls", LS)
@@ -246,7 +248,8 @@ def test_full_size_properties(gpu, oracle_lib, ls):
     assert solved.mean() > 0.99
     assert np.all(r["y"][solved] > 0) and np.all(r["s"][solved] > 0)
     assert np.all(r["newton_iters"] <= (20 - 1) * (r["outer_iters"] - 1))
-    bits = ((r["active_mask"][:, None] >> np.arange(m)) & 1).astype(bool)
+    assert r["active_mask"].shape == (B, 1)  # (B, W) on every path
+    bits = ((r["active_mask"] >> np.arange(m)) & 1).astype(bool)
     np.testing.assert_array_equal(bits, r["y"] > r["s"])
     idx = np.random.default_rng(0).choice(B, 96, replace=False)
     th = theta[idx].cpu().numpy()
