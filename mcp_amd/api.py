@@ -335,6 +335,15 @@ class PrimalDualMCP:
         return self
 
     @classmethod
+    def from_text(cls, path: str, compute_sensitivities=True, backend_options=None) -> "PrimalDualMCP":
+        """The MCP of a GH text file (mcp_amd/symtext.py): G/H printed by the Julia side from
+        its Symbolics expressions (src/mcp.jl:55-70), read back in the front end's symbols."""
+        from . import symtext
+
+        G, H, xs, ys, ts = symtext.load(path)
+        return cls.from_symbolic(G, H, xs, ys, ts, compute_sensitivities, backend_options)
+
+    @classmethod
     def from_symbolic_K(cls, K_symbolic, z_symbolic, θ_symbolic, lower_bounds, upper_bounds,
                         compute_sensitivities=True, backend_options=None) -> "PrimalDualMCP":
         self = cls()

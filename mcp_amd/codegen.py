@@ -185,8 +185,20 @@ class NLSystem:
         sp = _sp()
         self.n, self.m, self.p = len(xs), len(ys), len(ts)
         n, m = self.n, self.m
-        self.G, self.H = [sp.sympify(e) for e in G], [sp.sympify(e) for e in H]
-        self.xs, self.ys, self.ts = list(xs), list(ys), list(ts)
+        # The variables are renamed by position (x00000…, y00000…, θ00000…) before anything is
+        # generated: sympy orders the terms of a sum by the names of their symbols, and that order
+        # is the generated code's op order.  So the module depends on G/H and the positions of the
+        # variables only, not on what a front end called them — the sympy tracer's x_1, λ̃_1, μ̃_1
+        # and the names in a GH text from Julia (mcp_amd/symtext.py) give the same code object.
+        canon = ([sp.Symbol(f"x{i:05d}", real=True) for i in range(n)],
+                 [sp.Symbol(f"y{k:05d}", real=True) for k in range(m)],
+                 [sp.Symbol(f"θ{t:05d}", real=True) for t in range(self.p)])
+        sub = dict(zip(list(xs) + list(ys) + list(ts), canon[0] + canon[1] + canon[2]))
+        if len(sub) != n + m + self.p:
+            raise ValueError("the decision variables and parameters must be distinct symbols")
+        self.G = [sp.sympify(e).xreplace(sub) for e in G]
+        self.H = [sp.sympify(e).xreplace(sub) for e in H]
+        self.xs, self.ys, self.ts = canon
         zset = set(self.xs) | set(self.ys)
         nn, nm = n * n, n * m
         self.OFF_P, self.OFF_Q, self.OFF_R = 0, nn, nn + nm
