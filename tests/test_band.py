@@ -113,6 +113,32 @@ def test_band_oracle_equals_full_lu_on_solved_games(oracle_lib, T, B, ref_mode, 
     assert rel.max() <= 1e-10
 
 
+@pytest.mark.slow
+def test_t10_band_and_workgroup_equal_the_full_700_dim_lu(oracle_lib):
+    """C4 at the reference benchmark's horizon (T = 10, benchmark/trajectory_game_benchmark.jl:38):
+    the band elimination (what AUTO runs) and the workgroup LU of the 200-dim S against the literal
+    LU of the full (n + 2m) = 700-dim ∇F + tol·I (src/solver.jl:81-83), on the first 48 games of
+    the bench's θ stream.  The dense run takes the games both other modes solve (47; no 931-step
+    dense solves).  On them every discrete output (status, outer and Newton counts, α traces,
+    active sets) is identical, and the iterates agree to ≤ 1e-10 relative (observed 4.3e-13 band,
+    1.2e-13 workgroup)."""
+    game, tp = _c4(10, 48)
+    nl = game.mcp.nl
+    run = lambda th, **kw: oracle_lib.solve_batch_nl(nl, th, tol=1e-6, nthreads=8, trace_len=TRACE, **kw)
+    r = {"band": run(tp, linear_solver="schur", kernel="band"),
+         "wg": run(tp, linear_solver="schur", kernel="workgroup")}
+    both = (r["band"]["status"] == 0) & (r["wg"]["status"] == 0)
+    idx = np.nonzero(both)[0]
+    assert len(idx) == 47
+    d = run(np.ascontiguousarray(tp[idx]), linear_solver="dense")
+    assert (d["status"] == 0).all()
+    for mode, a in r.items():
+        for k in ("status", "outer_iters", "newton_iters", "active_mask", "alpha_trace"):
+            np.testing.assert_array_equal(a[k][idx], d[k], err_msg=f"{mode} {k}")
+        rel = np.abs(_z(a)[idx] - _z(d)).max(1) / np.maximum(1.0, np.abs(_z(d)).max(1))
+        assert rel.max() <= 1e-10, (mode, rel.max())
+
+
 def test_band_mode_follows_the_kernel_choice(oracle_lib):
     """AUTO takes the band kernel at T = 10 (no one-wave SCHUR kernel: n = 200) and the one-wave
     Gauss-Jordan at T = 2 (the module does not prefer the band kernel there); the oracle picks its
