@@ -201,6 +201,11 @@ void mcpx_default_params(mcpx_params* prm);
 int64_t mcpx_theta_dim(int32_t family, int32_t n, int32_t m);
 /* number of visible HIP devices (0 when none) */
 int mcpx_device_count(void);
+/* Debug: with MCPX_POISON=1 in the environment every device block the library allocates for
+ * itself is filled with NaN bytes up to its requested size and a canary after it, checked when
+ * the block is released; this returns the number of blocks found overwritten past their size
+ * (each also reported on stderr).  0 without MCPX_POISON. */
+int64_t mcpx_debug_canary_violations(void);
 
 /* Host-buffer batched solve (what the Julia ccall / Python API drive).
  * Copies θ (and optional warm starts x0/y0/s0, each [B*n] / [B*m], NULL ⇒

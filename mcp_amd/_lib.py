@@ -31,7 +31,8 @@ EXPORTS = ("mcpx_version", "mcpx_last_error", "mcpx_default_params", "mcpx_theta
            "mcpx_module_dims", "mcpx_module_unload", "mcpx_solve_batch_module", "mcpx_solve_batch_module_device",
            "mcpx_host_register", "mcpx_host_unregister", "mcpx_vjp_batch_module", "mcpx_vjp_batch_module_device",
            "mcpx_jvp_batch_module", "mcpx_jvp_batch_module_device", "mcpx_solve_vjp_batch_device",
-           "mcpx_cond_batch", "mcpx_cond_batch_device", "mcpx_cond_batch_module", "mcpx_cond_batch_module_device")
+           "mcpx_cond_batch", "mcpx_cond_batch_device", "mcpx_cond_batch_module", "mcpx_cond_batch_module_device",
+           "mcpx_debug_canary_violations")
 
 
 ABI_MAJOR = 2  # include/mcpx.h MCPX_VERSION / 10000
@@ -54,6 +55,7 @@ def lib():
     L.mcpx_theta_dim.restype = C.c_int64
     L.mcpx_theta_dim.argtypes = [C.c_int32, C.c_int32, C.c_int32]
     L.mcpx_device_count.restype = C.c_int
+    L.mcpx_debug_canary_violations.restype = C.c_int64
     L.mcpx_solve_batch.restype = C.c_int
     L.mcpx_solve_batch.argtypes = [C.POINTER(_abi.Desc), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                    C.POINTER(_abi.Params), C.c_int, C.POINTER(_abi.Out)]

@@ -78,15 +78,23 @@ def _affine_rows(rows: list, zs: list, what: str):
     C, c = [], []
     for i, e in enumerate(rows):
         e = sp.expand(e)
+        # the polynomial in the variables this row uses only (a Poly over all n + m generators is
+        # a recursion as deep as their number: past ~1,000 it overflows, e.g. the lane change at T = 30)
+        # (the coefficients of the other variables: the zero of the polynomial's domain, as
+        # coeff_monomial gives over all generators — e.g. Float 0.0 for a row with float
+        # constants, which the QP / affine classification then sees exactly as before)
         if zs:
+            fs = e.free_symbols
+            used = [z for z in zs if z in fs]
             try:
-                poly = sp.Poly(e, *zs)
+                poly = sp.Poly(e, *(used or zs[:1]))
             except sp.PolynomialError as exc:
                 raise NotAffineError(f"{what}[{i}] is not polynomial in the decision variables: {e}") from exc
             if poly.total_degree() > 1:
                 raise NotAffineError(f"{what}[{i}] is not affine in the decision variables (degree "
                                      f"{poly.total_degree()}); general nonlinear G/H is SURVEY.md §8(f) #2")
-            C.append([poly.coeff_monomial(z) for z in zs])
+            zero = poly.domain.to_sympy(poly.domain.zero)
+            C.append([poly.coeff_monomial(z) if z in fs else zero for z in zs])
             c.append(poly.coeff_monomial(1))
         else:
             C.append([])

@@ -81,9 +81,12 @@ _MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_nl_band.hpp", "ipm_kernel_impl.hpp", "
                 "ipm_wg_impl.hpp", "lu_vr.hpp", "sens_wg_impl.hpp", "sens_kernel.h", "../../include/mcpx.h")
 WG_LDS_LIMIT = 160 * 1024 - 2048  # MCPX_NL_WG_LIMIT of csrc/ipm_nl_kernel.hpp
 LDS_LIMIT = 160 * 1024 - 2048  # bytes of static LDS one workgroup may declare on gfx950 (minus headroom)
-# band kernel (csrc/ipm_nl_band.hpp): four instances per CU (the C4 batch of 1,024 games on 256
-# CUs) need ≤ 40 KB of LDS each
-BAND_LDS_LIMIT = 40 * 1024
+# band kernel (csrc/ipm_nl_band.hpp): as much LDS as one workgroup may declare.  The launch sizes
+# its persistent grid by the kernel's occupancy (mcpx_api.cpp launch_band), so a longer horizon
+# runs fewer games per CU at once (T = 10: 40 KB, four per CU; T = 15: 60 KB, two) rather than
+# falling back to the workgroup LU — a tail-bound launch (the 931-step failing games set its
+# length) loses little by it
+BAND_LDS_LIMIT = LDS_LIMIT
 BAND_KERNEL = True  # the band kernel is compiled into modules (csrc/ipm_nl_band.hpp)
 
 _FUNCS = {  # sympy function → C name (both libm and HIP device math)

@@ -160,8 +160,9 @@ static_assert(WC % UD == 0 && EMAX <= 64, "band tables");
 // 2n doubles), so the back substitution's entering rows come from LDS, not from branch-guarded
 // loads (see factor_solve).
 constexpr bool BSL = !ULDS && MCPX_BAND_BS_NOBR;
-static_assert(8 * (EVN + NNZ + 1 + n + 2 * m + n + 2 * WC + (ULDS ? n * US : 0) + (BSL ? 2 * n : 0)) <= 40 * 1024,
-              "band kernel LDS (mcp_amd/band.py BandPlan.lds_bytes)");
+static_assert(8 * (EVN + NNZ + 1 + n + 2 * m + n + 2 * WC + (ULDS ? n * US : 0) + (BSL ? 2 * n : 0)) <=
+                  160 * 1024 - 2048,
+              "band kernel LDS (mcp_amd/band.py BandPlan.lds_bytes, codegen.BAND_LDS_LIMIT)");
 
 struct Win {
   double acc[NJ][NCB], rh[NJ];

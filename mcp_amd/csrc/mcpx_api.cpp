@@ -432,12 +432,58 @@ bool outputs_ok(const mcpx_out* o) {
 // HIP calls during teardown).
 constexpr uint64_t kCacheKeep = 4ull << 30;
 
+// MCPX_POISON=1 (debug): every block handed out is filled with 0xFF bytes (NaN doubles) up to
+// the requested size, and the rest of the block (at least kCanary bytes) with the canary byte
+// 0xA5.  At release the tail is read back and checked: a write past the requested size is
+// reported on stderr ("MCPX_POISON canary") and counted (mcpx_debug_canary_violations), and a
+// kernel result that depended on workspace read before it was written turns NaN or changes.
+// Host synchronisation at every release: a diagnostic mode, not for timing.
+constexpr size_t kCanary = 4096;
+constexpr unsigned char kCanaryByte = 0xA5;
+std::atomic<int64_t> g_canary_bad{0};
+
+bool poison_on() {
+  static const bool on = [] {
+    const char* v = std::getenv("MCPX_POISON");
+    return v && std::atoi(v) == 1;
+  }();
+  return on;
+}
+
 struct Block {
   void* p = nullptr;
   size_t bytes = 0;
+  size_t req = 0;             // MCPX_POISON: the size requested by the current user
   hipEvent_t last = nullptr;  // recorded after the block's last use
   bool busy = false;
 };
+
+// MCPX_POISON: fill a block just handed out (stream-ordered)
+hipError_t poison_block(Block& b, size_t bytes, hipStream_t st) {
+  b.req = bytes;
+  hipError_t e = hipMemsetAsync(b.p, 0xFF, bytes, st);
+  if (e == hipSuccess) e = hipMemsetAsync((char*)b.p + bytes, kCanaryByte, b.bytes - bytes, st);
+  return e;
+}
+
+// MCPX_POISON: check a block's tail after its last use on `st` (host-synchronising)
+void check_canary(const Block& b, hipStream_t st) {
+  const size_t tail = b.bytes - b.req;
+  std::vector<unsigned char> h(tail);
+  if (hipMemcpyAsync(h.data(), (const char*)b.p + b.req, tail, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    std::fprintf(stderr, "MCPX_POISON canary: could not read back block %p\n", b.p);
+    g_canary_bad.fetch_add(1);
+    return;
+  }
+  for (size_t i = 0; i < tail; ++i)
+    if (h[i] != kCanaryByte) {
+      std::fprintf(stderr, "MCPX_POISON canary: block %p (%zu bytes requested, %zu held) overwritten at +%zu\n",
+                   b.p, b.req, b.bytes, b.req + i);
+      g_canary_bad.fetch_add(1);
+      return;
+    }
+}
 
 struct BlockCache {
   std::mutex mu;
@@ -454,7 +500,8 @@ hipError_t dev_alloc(void** p, size_t bytes, hipStream_t st) {
   int d = 0;
   hipError_t e = hipGetDevice(&d);
   if (e != hipSuccess) return e;
-  const size_t want = (std::max<size_t>(bytes, 1) + (2u << 20) - 1) / (2u << 20) * (2u << 20);  // 2 MiB granules
+  const size_t need = std::max<size_t>(bytes, 1) + (poison_on() ? kCanary : 0);
+  const size_t want = (need + (2u << 20) - 1) / (2u << 20) * (2u << 20);  // 2 MiB granules
   BlockCache& c = block_cache();
   std::lock_guard<std::mutex> lock(c.mu);
   auto& v = c.dev[d];
@@ -463,6 +510,7 @@ hipError_t dev_alloc(void** p, size_t bytes, hipStream_t st) {
     if (!b.busy && b.bytes >= want && b.bytes <= 2 * want && (!best || b.bytes < best->bytes)) best = &b;
   if (best) {
     if (best->last && (e = hipStreamWaitEvent(st, best->last, 0)) != hipSuccess) return e;
+    if (poison_on() && (e = poison_block(*best, bytes, st)) != hipSuccess) return e;
     best->busy = true;
     *p = best->p;
     return hipSuccess;
@@ -480,6 +528,7 @@ hipError_t dev_alloc(void** p, size_t bytes, hipStream_t st) {
     (void)hipGetLastError();
     if ((e = hipMalloc(&b.p, want)) != hipSuccess) return e;
   }
+  if (poison_on() && (e = poison_block(b, bytes, st)) != hipSuccess) return e;
   b.busy = true;
   v.push_back(b);
   *p = b.p;
@@ -493,6 +542,7 @@ void dev_release(void* p, hipStream_t st) {
   for (auto& [d, v] : c.dev) {
     for (auto& b : v) {
       if (b.p != p) continue;
+      if (poison_on()) check_canary(b, st);
       if (!b.last) (void)hipEventCreateWithFlags(&b.last, hipEventDisableTiming);
       if (b.last) (void)hipEventRecord(b.last, st);
       b.busy = false;
@@ -1204,6 +1254,8 @@ int mcpx_device_count(void) {
   if (hipGetDeviceCount(&c) != hipSuccess) return 0;
   return c;
 }
+
+int64_t mcpx_debug_canary_violations(void) { return g_canary_bad.load(); }
 
 int mcpx_solve_batch_device(const mcpx_desc* d, const double* theta, const double* x0, const double* y0,
                             const double* s0, const mcpx_params* prm, const mcpx_out* o, void* stream) {

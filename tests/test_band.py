@@ -208,6 +208,26 @@ def test_gpu_band_t10(gpu, oracle_lib, B, warm):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("T", [12, 15])
+def test_gpu_band_past_the_benchmark_horizon(gpu, oracle_lib, T):
+    """Past T = 10 the band kernel's LDS grows (48 KB at T = 12, 60 KB at T = 15): it still runs,
+    with fewer games per CU (the launch sizes its grid by occupancy), instead of AUTO falling back
+    to the workgroup LU (the research application runs horizon 30,
+    examples/train_and_test_utils.jl:585).  AUTO takes it, bit-exact against lu_band_solve."""
+    from mcp_amd.batch import solve_batch
+    from tests.test_gpu_parity import assert_parity
+
+    game, tp = _c4(T, 32)
+    mcp = game.mcp
+    assert mcp.nl.band_can and mcp.nl.band_auto
+    got = solve_batch(_abi.FAMILY_NONLINEAR, mcp.nl.n, mcp.nl.m, tp, linear_solver="schur", trace_len=TRACE,
+                      module=mcp.module())
+    ref = oracle_lib.solve_batch_nl(mcp.nl, tp, linear_solver="schur", trace_len=TRACE, nthreads=8)
+    assert_parity(got, ref)
+    assert (ref["status"] == 0).mean() > 0.8
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("runtime", ["torch", "system"])
 def test_gpu_host_calls_repeat_bit_exact(gpu, oracle_lib, runtime):
     """Back-to-back host-buffer calls in one process (T = 10, 1,024 games): every call bit-exact
@@ -239,6 +259,28 @@ def test_gpu_host_calls_repeat_bit_exact(gpu, oracle_lib, runtime):
         got = solve_batch(_abi.FAMILY_NONLINEAR, mcp.nl.n, mcp.nl.m, batches[call % 2], linear_solver="schur",
                           trace_len=TRACE, module=mcp.module())
         assert_parity(got, refs[call % 2])
+
+
+@pytest.mark.gpu
+def test_gpu_host_calls_repeat_poisoned(gpu):
+    """the repeated host calls of the system-runtime case once more with
+    MCPX_POISON=1 — every library block handed out NaN-filled up to its requested size, a canary
+    after it checked at release.  A kernel that read workspace before writing it would change its
+    games, one that wrote past a block's end would trip the canary: all 6 calls stay bit-exact
+    against the oracle with every canary intact, so the wrong games of the HIP 7.2 pool were not
+    a kernel-side read or write."""
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k != "PYTHONPATH"}
+    env["MCPX_POISON"] = "1"
+    p = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tools", "band_stress.py"), "10", "1024", "band",
+                        "6", "reuse"], capture_output=True, text=True, timeout=200, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "MCPX_POISON canary" not in p.stderr, p.stderr[-2000:]
+    calls = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(calls) == 6 and all(c["vs_oracle"] == 0 and c["canary"] == 0 for c in calls), calls
 
 
 @pytest.mark.gpu

@@ -6,7 +6,8 @@ kernel: band | workgroup | auto; reuse: one Module for every call; reload: a new
 (solve_batch_device); pinned: one Module, θ page-locked.  hsaco: a tools/bandv build instead of
 the module cache's.  Each call is compared with the oracle and with call 0.
 STRESS_FLUSH=1: a 512 MiB device fill between calls (evicts the L2s); STRESS_ALT=1: odd calls solve
-a second parameter batch (compared with its own oracle solution)."""
+a second parameter batch (compared with its own oracle solution).  MCPX_POISON=1: the library's
+device blocks come NaN-filled with a checked canary after them ("canary" = blocks overwritten)."""
 import json, os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -101,7 +102,10 @@ for i in range(count):
         det.append([int(b), int(r["newton_iters"][b]), int(ref["newton_iters"][b]), int(r["status"][b]),
                     int(dif[0]) if len(dif) else -1, fields, other,
                     float(r["kkt_error"][b]), float(ref["kkt_error"][b]), float(r["eps"][b]), float(ref["eps"][b])])
+    from mcp_amd._lib import lib as _mcpx
+
     print(json.dumps({"call": i, "s": round(dt, 4), "vs_oracle": int(vo.sum()), "vs_call0": int(v0.sum()),
+                      "canary": int(_mcpx().mcpx_debug_canary_violations()),
                       "first_bad": np.nonzero(v0 if v0.any() else vo)[0][:8].tolist(),
                       "newton": int(r["newton_iters"].sum()), "bad[inst,newton,ref,status,step]": det}), flush=True)
 print("oracle newton", int(ref["newton_iters"].sum()), flush=True)
