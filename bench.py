@@ -45,7 +45,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector = FP64 matrix peak (MI355X_MICROAR
 HBM_PEAK_GBS = 8000.0
 XCDS, SIMDS = 8, 256 * 4  # MI355X: 8 XCDs, 256 CUs × 4 SIMDs
 # rocprofv3 evidence of this round's kernels (tools/gpu_profile.sh + tools/prof_summary.py)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
+PROFILE_DIR = os.environ.get("MCPX_PROFILE_DIR") or os.path.join(ROOT, "profiles", "r06")
 DEFAULT_GLOBAL = {"c3": 65536, "c5": 4096, "c4": 1024}
 QP_FIELDS = ("x", "y", "s", "kkt_error", "eps", "outer_iters", "status", "newton_iters")
 C4_FIELDS = QP_FIELDS
@@ -280,7 +280,7 @@ def launch_ranks(nranks: int, script: str, argv, have_devices: int | None = None
 
 
 def evidence(name: str, cfg: dict) -> dict:
-    """The committed rocprofv3 summaries of this configuration (profiles/r05/
+    """The committed rocprofv3 summaries of this configuration (profiles/r06/ or MCPX_PROFILE_DIR:
     trace_<name>.json, pmc_<name>.json; tools/prof_summary.py), if they were taken on
     exactly this configuration and this build of libmcpx.so; else {}."""
     from mcp_amd.build import built_hash
@@ -388,14 +388,32 @@ def reduce_max_sum(dist, dev, world, maxes, sums):
 
 def roofline(kern_ms: float, flops_launch: float, exec_flops_launch: float, alg_bytes: float, ev: dict,
              kernel: str, bound, note: str) -> dict:
+    """The line's roofline record.  `frac` is SURVEY.md §8(d)'s: the dense-LU FLOPs of the full KKT
+    system per Newton step over the kernel time.  A fraction above 1 means that count is not a
+    roofline for the kernel (an exact elimination that skips structural zeros — the generated
+    modules' band and Schur solves, as the reference's sparse UMFPACK does): `frac` is then the
+    structural count (the elimination the kernel performs, `executed`), and the dense figure is
+    kept as `frac_dense_kkt` with `dense_count_exceeds_peak`.  A fraction above 1 on the
+    structural count too is an error in the line (`frac` null, `frac_error`)."""
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12
     executed = exec_flops_launch / (kern_ms * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(ev)
     bound, bound_ev = bound
+    basis = ("algorithmic: SURVEY.md §8(d) dense-LU FLOPs of the full KKT system (not the FLOPs the "
+             "kernel executes: executed_frac)")
+    dense_frac = achieved / FP64_PEAK_TFLOPS
+    extra = {}
+    if dense_frac > 1.0:
+        extra = {"frac_dense_kkt": dense_frac, "dense_count_exceeds_peak": True}
+        achieved = executed
+        basis = ("structural: the FLOPs of the elimination the kernel performs (the dense KKT count exceeds "
+                 "the FP64 peak, so it is not a roofline for this kernel: frac_dense_kkt)")
+    frac = achieved / FP64_PEAK_TFLOPS
+    if frac > 1.0:
+        extra["frac_error"] = f"structural FLOPs over the kernel time exceed the FP64 peak ({frac:.3f})"
+        frac = None
     r = {"bound": bound, "bound_evidence": bound_ev, "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-         "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-         "frac_basis": "algorithmic: SURVEY.md §8(d) dense-LU FLOPs of the full KKT system (not the FLOPs the "
-                       "kernel executes: executed_frac)",
+         "unit": "TFLOP/s", "frac": frac, "frac_basis": basis, **extra,
          "traffic": traffic, "traffic_source": traffic_src,
          "executed_tflops": executed, "executed_frac": executed / FP64_PEAK_TFLOPS,
          "algorithmic_bytes": alg_bytes, "hbm_gbs_algorithmic": alg_bytes / (kern_ms * 1e-3) / 1e9,
@@ -404,7 +422,8 @@ def roofline(kern_ms: float, flops_launch: float, exec_flops_launch: float, alg_
     tr = ev.get("trace")
     if tr:
         t_ms = float(tr.get("launch_avg_ms_all_passes", tr["avg_ms"]))
-        r.update(trace_kernel_ms=t_ms, frac_trace=flops_launch / (t_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+        num = exec_flops_launch if extra.get("dense_count_exceeds_peak") else flops_launch
+        r.update(trace_kernel_ms=t_ms, frac_trace=num / (t_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                  executed_frac_trace=exec_flops_launch / (t_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                  trace_source=tr["_source"])
     if traffic:
@@ -494,6 +513,29 @@ def main_lane_change(a, world, rank, local, dist, pl):
                   f"{mcp.nl.band.wc}" if bandk else f"LU of dim {solve_dim(n, m, ls)}") +
                   (" + the Schur complement from Q's structural nonzeros" if ls == "schur" else "") +
                   "); bound: per-wave latency (PMC: waves stall on LDS/VALU dependencies, DESIGN.md §4)")
+    rl["frac_structural"] = rl["executed_frac"]
+    # critical path: the game with the most Newton steps solved alone (one wave on an idle GPU,
+    # the same kernel): its time over the launch's says how much of the launch is that one
+    # game's chain of dependent steps (≈ 1: tail-bound, the rest of the batch fits beside it)
+    imax = int(torch.argmax(out["newton_iters"]).item())
+    nmax = int(out["newton_iters"][imax].item())
+    one = alloc_device_outputs(1, n, m, dev)
+    th1 = theta[imax:imax + 1].contiguous()
+    lone = []
+    for rep in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        solve_batch_device(_abi.FAMILY_NONLINEAR, n, m, th1, one, tol=a.tol, linear_solver=ls, stream=stream,
+                           module=module, kernel=a.kernel)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        if rep:
+            lone.append(e0.elapsed_time(e1))
+    lone_ms = float(np.mean(lone))
+    rl["critical_path"] = {"longest_game_newton": nmax, "lone_game_ms": lone_ms,
+                           "lone_step_us": lone_ms * 1e3 / max(nmax, 1), "frac_of_launch": lone_ms / kern_ms,
+                           "note": "the longest game of rank 0's batch solved alone (B = 1, same kernel) over the "
+                                   "batch launch's kernel time: the share of the launch its dependent chain sets"}
     res = {
         "metric": ("MCP solve+VJP/sec (lane-change trajectory game, generated nonlinear module, rrule pullback of "
                    "x₁ as examples/utils.jl:236-261)" if a.sens else
@@ -669,7 +711,7 @@ def main_qp(a, world, rank, local, dist, pl, distributed):
     rl = roofline(kern_ms, newton * lu_flops(N), newton * executed_flops(n, m, ls),
                   B * (8.0 * (p + n + 2 * m + 2) + 12.0), ev,
                   "ipm_solve_kernel" if one_wave(n, m, ls) else "ipm_wg",  # ipm_wg_kernel_t / ipm_wg_vr_kernel_t
-                  roofline_bound(ev, kern_ms, "valu" if one_wave(n, m, ls) else "hbm"),
+                  roofline_bound(ev, kern_ms, "valu" if one_wave(n, m, ls) else "latency"),
                   f"achieved = SURVEY.md §8(d) algorithmic FLOPs (dense LU of the N={N} KKT system, 2N^3/3+2N^2 per "
                   f"Newton step) x rank 0's own Newton counts / HIP-event time of the solve launch; executed = the FP64 "
                   f"work the kernel performs per step (residual + " + ("MFMA Schur complement + Gauss-Jordan of the "

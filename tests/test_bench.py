@@ -124,10 +124,26 @@ def test_evidence_only_for_its_config_and_build(tmp_path, monkeypatch):
     assert bench.evidence("x", cfg) == {}  # another build of libmcpx.so
 
 
+def test_roofline_frac_never_exceeds_peak():
+    """A dense §8(d) count above the FP64 peak is not a roofline for the kernel:
+    `frac` falls back to the structural count (the elimination the kernel performs) and the dense
+    figure is flagged; a structural count above the peak too makes `frac` null with an error."""
+    import bench
+
+    peak_flops_ms = bench.FP64_PEAK_TFLOPS * 1e12 * 1e-3  # FLOPs in 1 ms at peak
+    r = bench.roofline(1.0, 0.5 * peak_flops_ms, 0.2 * peak_flops_ms, 1e9, {}, "k", ("latency", {}), "")
+    assert r["frac"] == pytest.approx(0.5) and "dense_count_exceeds_peak" not in r
+    r = bench.roofline(1.0, 1.02 * peak_flops_ms, 0.0015 * peak_flops_ms, 1e9, {}, "k", ("latency", {}), "")
+    assert r["frac"] == pytest.approx(0.0015) and r["dense_count_exceeds_peak"]
+    assert r["frac_dense_kkt"] == pytest.approx(1.02) and r["frac_basis"].startswith("structural")
+    r = bench.roofline(1.0, 2.0 * peak_flops_ms, 1.5 * peak_flops_ms, 1e9, {}, "k", ("latency", {}), "")
+    assert r["frac"] is None and "frac_error" in r
+
+
 def test_committed_evidence_is_self_consistent():
     """Every committed profiles/r0x trace/PMC summary names its configuration and
     build, and a bench line committed beside it quotes the same kernel time within 2 %."""
-    dirs = [os.path.join(ROOT, "profiles", r) for r in ("r02", "r03")]
+    dirs = [os.path.join(ROOT, "profiles", r) for r in ("r02", "r03", "r06")]
     files = [(d, f) for d in dirs if os.path.isdir(d) for f in sorted(os.listdir(d))]
     if not files:
         pytest.skip("no profiles yet")

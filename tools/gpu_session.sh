@@ -9,6 +9,7 @@
 #   driver                the driver's bench command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   bench=<name>:<args>   one bench line, args comma-separated (bench=c4:--lane-change,2)
 #   prof=<name>:<args>    tools/gpu_profile.sh: bench line + rocprofv3 trace + PMC passes
+#   evid=<name>:<args>    tools/evidence.sh: prof, summaries, then the bench line quoting them
 #   timeline=<args>       tools/timeline.py (residency timeline of a SCHUR launch), args comma-separated
 #   probe=<name>          tools/parity_probe.py (C3, C2 shapes) on the variant tools/ablib/libmcpx_<name>.so
 #   shard                 the per-GPU shards of the strong-scaling configs (C3 2/4/8, C5 512, C4 128)
@@ -47,6 +48,10 @@ for step in "$@"; do
       spec=${step#prof=}; name=${spec%%:*}; args=${spec#*:}
       [ "$args" = "$spec" ] && args=""
       bash tools/gpu_profile.sh "$name" ${args//,/ } || exit 7 ;;
+    evid=*)
+      spec=${step#evid=}; name=${spec%%:*}; args=${spec#*:}
+      [ "$args" = "$spec" ] && args=""
+      bash tools/evidence.sh "$name" ${args//,/ } || exit 11 ;;
     timeline=*)
       args=${step#timeline=}
       timeout -k 10 300 python -u tools/timeline.py ${args//,/ } --out "$O" > "$O/timeline.log" 2>&1 || { tail -20 "$O/timeline.log"; exit 9; }
