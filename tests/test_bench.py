@@ -138,6 +138,9 @@ def test_roofline_frac_never_exceeds_peak():
     assert r["frac_dense_kkt"] == pytest.approx(1.02) and r["frac_basis"].startswith("structural")
     r = bench.roofline(1.0, 2.0 * peak_flops_ms, 1.5 * peak_flops_ms, 1e9, {}, "k", ("latency", {}), "")
     assert r["frac"] is None and "frac_error" in r
+    r = bench.roofline(1.0, 0.99 * peak_flops_ms, 0.002 * peak_flops_ms, 1e9, {}, "k", ("latency", {}), "",
+                       structural=True)  # a generated module's line: the structural basis always
+    assert r["frac"] == pytest.approx(0.002) and not r["dense_count_exceeds_peak"]
 
 
 def test_committed_evidence_is_self_consistent():
