@@ -22,6 +22,7 @@ FAMILY_NONLINEAR = 2  # generated device code per problem (mcp_amd/codegen.py)
 
 MAX_KKT_DIM = 64
 MAX_WG_KKT_DIM = 768  # MCPX_MAX_WG_KKT_DIM: workgroup-per-instance kernels (QP / affine)
+MAX_WG_SCHUR_N = 128  # wg::kGjMax: the QP family's workgroup SCHUR kernels (csrc/gj_vr.hpp)
 KERNEL_AUTO, KERNEL_WAVE, KERNEL_WORKGROUP, KERNEL_MULTIWAVE, KERNEL_BAND = 0, 1, 2, 3, 4
 KERNELS = {"auto": KERNEL_AUTO, "wave": KERNEL_WAVE, "workgroup": KERNEL_WORKGROUP, "multiwave": KERNEL_MULTIWAVE,
            "band": KERNEL_BAND}

@@ -562,12 +562,14 @@ def _linear_solver(mcp: PrimalDualMCP, linear_solve_algorithm) -> str:
     if linear_solve_algorithm is None:
         if mcp.family == _abi.FAMILY_NONLINEAR:
             return mcp.nl.default_solver()
-        # the MFMA Schur-complement kernel for the QP family (one wave: n + m ≤ 64).  An
-        # affine-family MCP here has −Q ≠ Rᵀ symbolically (else it is classified QP), so its
-        # SCHUR solve would always take the pivoting-LU pass, whose rate is not the measured
-        # one: REDUCED (pivoting over the whole n + m system) stays its default.
-        one_wave = mcp.unconstrained_dimension + mcp.constrained_dimension <= _abi.MAX_KKT_DIM
-        return "schur" if mcp.family == _abi.FAMILY_QP and one_wave else "reduced"
+        # the MFMA Schur-complement kernels for the QP family (one wave: n + m ≤ 64; one
+        # workgroup: n ≤ 128, csrc/gj_vr.hpp).  An affine-family MCP here has −Q ≠ Rᵀ
+        # symbolically (else it is classified QP), so its SCHUR solve would always take the
+        # pivoting-LU pass, whose rate is not the measured one: REDUCED (pivoting over the
+        # whole n + m system) stays its default.
+        n, m = mcp.unconstrained_dimension, mcp.constrained_dimension
+        schur_ok = n + m <= _abi.MAX_KKT_DIM or (n <= _abi.MAX_WG_SCHUR_N and n + 2 * m <= _abi.MAX_WG_KKT_DIM)
+        return "schur" if mcp.family == _abi.FAMILY_QP and schur_ok else "reduced"
     if isinstance(linear_solve_algorithm, str):
         if linear_solve_algorithm not in _abi.LINEAR_SOLVERS:
             raise ValueError(f"linear_solve_algorithm must be one of {sorted(_abi.LINEAR_SOLVERS)}")

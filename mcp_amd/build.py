@@ -27,7 +27,7 @@ LIB = os.path.join(HERE, "libmcpx.so")
 SOURCES = [os.path.join(CSRC, f) for f in (
     "ipm_inst_red_qp.hip", "ipm_inst_spec.hip", "ipm_inst_schur_qp.hip", "ipm_inst_schur_aff.hip", "ipm_inst_red_aff.hip",
     "ipm_inst_dense_qp.hip", "ipm_inst_dense_aff.hip", "sens_inst_vjp.hip", "sens_inst_jvp.hip",
-    "ipm_inst_wg.hip", "ipm_inst_wg_vr.hip", "sens_inst_wg.hip", "ipm_inst_fused.hip", "mcpx_api.cpp")]
+    "ipm_inst_wg.hip", "ipm_inst_wg_vr.hip", "ipm_inst_wg_gj.hip", "sens_inst_wg.hip", "ipm_inst_fused.hip", "mcpx_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("ipm_kernel.h", "ipm_kernel_impl.hpp", "bcast_group.inc", "sens_kernel.h", "sens_kernel_impl.hpp",
     "ipm_wg.h", "ipm_wg_impl.hpp", "lu_vr.hpp", "sens_wg_impl.hpp")] + [
     os.path.join(ROOT, "include", "mcpx.h")]

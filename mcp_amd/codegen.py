@@ -78,7 +78,7 @@ EVAL_PARTS = 4  # mcpx_nl_eval_p0..p3: the generated eval split over the 4-wave 
 _MODULE_FLAGS = ("--genco", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", "-Wno-unused-function",
                  "-mllvm", "-amdgpu-mfma-vgpr-form=1")
 _MODULE_DEPS = ("ipm_nl_kernel.hpp", "ipm_nl_band.hpp", "ipm_kernel_impl.hpp", "ipm_kernel.h", "bcast_group.inc", "ipm_wg.h",
-                "ipm_wg_impl.hpp", "lu_vr.hpp", "sens_wg_impl.hpp", "sens_kernel.h", "../../include/mcpx.h")
+                "ipm_wg_impl.hpp", "lu_vr.hpp", "gj_vr.hpp", "sens_wg_impl.hpp", "sens_kernel.h", "../../include/mcpx.h")
 WG_LDS_LIMIT = 160 * 1024 - 2048  # MCPX_NL_WG_LIMIT of csrc/ipm_nl_kernel.hpp
 LDS_LIMIT = 160 * 1024 - 2048  # bytes of static LDS one workgroup may declare on gfx950 (minus headroom)
 # band kernel (csrc/ipm_nl_band.hpp): as much LDS as one workgroup may declare.  The launch sizes

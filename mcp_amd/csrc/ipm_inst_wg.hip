@@ -33,6 +33,8 @@ const void* ipm_wg_kernel(int family, int solver, int nv, int ns) {
       return qp ? pick<MCPX_FAMILY_QP, MCPX_LINSOLVE_REDUCED>(nv, ns) : pick<MCPX_FAMILY_AFFINE, MCPX_LINSOLVE_REDUCED>(nv, ns);
     case MCPX_LINSOLVE_DENSE:
       return qp ? pick<MCPX_FAMILY_QP, MCPX_LINSOLVE_DENSE>(nv, ns) : pick<MCPX_FAMILY_AFFINE, MCPX_LINSOLVE_DENSE>(nv, ns);
+    case MCPX_LINSOLVE_SCHUR:  // the QP family, n ≤ 128 (gj_vr.hpp)
+      return qp && ns <= wg::kGjMax ? ipm_wg_gj_kernel(nv) : nullptr;
     default:
       return nullptr;
   }

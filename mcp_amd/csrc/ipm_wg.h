@@ -47,6 +47,7 @@ struct WgSensArgs {
 constexpr int kThreads = 256;       // workgroup size of every workgroup kernel (4 waves)
 constexpr int kMaxDim = 768;        // largest system / vector dimension of the QP / affine kernels
 constexpr int kDimBuckets[4] = {128, 256, 512, 768};
+constexpr int kGjMax = 128;         // largest n of the QP family's workgroup SCHUR kernels (gj_vr.hpp)
 
 }  // namespace wg
 
@@ -59,6 +60,8 @@ const void* ipm_wg_kernel(int family, int solver, int nv, int ns);
 // The register-resident ones (ipm_inst_wg_vr.hip): bucket 128, and bucket 256 for
 // systems of at most MCPX_VR_MAX rows; nullptr otherwise.
 const void* ipm_wg_vr_kernel(int family, int solver, int nv);
+// The QP family's MCPX_LINSOLVE_SCHUR for n ≤ wg::kGjMax (ipm_inst_wg_gj.hip); nullptr otherwise.
+const void* ipm_wg_gj_kernel(int nv);
 hipError_t launch_ipm_wg(int family, int solver, int nv, int ns, const wg::WgArgs& a, int grid, hipStream_t st);
 // Sensitivity kernels of the QP and affine families beyond the one-wave kernels'
 // 64 rows (sens_inst_wg.hip): VJP (jvp = false) or JVP at vector dimension

@@ -399,6 +399,7 @@ __device__ __forceinline__ bool lu_solve(double* __restrict__ A, int ld, int ns,
 }  // namespace mcpx
 
 #include "lu_vr.hpp"  // the register-resident LU (uses the helpers above)
+#include "gj_vr.hpp"  // the QP family's SCHUR step: MFMA Schur complement + blocked Gauss-Jordan
 
 namespace mcpx {
 namespace wg {
@@ -500,6 +501,12 @@ __device__ __forceinline__ double jac(const double* __restrict__ th, const doubl
   return 0.0;
 }
 
+// MCPX_WG_TWICE (diagnostic builds only, tools/ab_build.py): 1 the register LU (lu_solve_vr)
+// of the QP / affine step runs twice, 2 the residual F — both idempotent (same bits, the added
+// time is the phase's cost).
+#ifndef MCPX_WG_TWICE
+#define MCPX_WG_TWICE 0
+#endif
 // Systems of up to MCPX_VR_MAX rows are factored in registers (lu_vr.hpp), larger ones
 // through the slot's HBM workspace (lu_solve above).
 #ifndef MCPX_VR_MAX
@@ -526,10 +533,18 @@ struct SePatch {
   }
 };
 
-template <int NVMAX, int NSMAX, bool VR = kVr<NSMAX>>
+// The QP SCHUR step (gj_vr.hpp) and its pivoting-LU fallback share their LDS: one or the other
+// is live.
+template <int NSMAX>
+union VrGjShared {
+  VrShared<NSMAX, 1> vr;
+  GjShared<NSMAX> gj;
+};
+
+template <int NVMAX, int NSMAX, bool VR = kVr<NSMAX>, bool GJ = false>
 struct SolveShared {
   double zs[NVMAX], Fs[NVMAX], dzs[NVMAX];
-  std::conditional_t<VR, VrShared<NSMAX, 1>, LuShared<NSMAX>> lu;
+  std::conditional_t<GJ, VrGjShared<NSMAX>, std::conditional_t<VR, VrShared<NSMAX, 1>, LuShared<NSMAX>>> lu;
   Scratch sc;
 };
 
@@ -537,8 +552,15 @@ template <int FAMILY, int SOLVER, int NVMAX, int NSMAX, class GEN>
 __device__ __forceinline__ void solve_instances(const WgArgs& W) {
   constexpr bool SCH = SOLVER == MCPX_LINSOLVE_SCHUR, RED = SOLVER == MCPX_LINSOLVE_REDUCED;
   constexpr bool NL = FAMILY == MCPX_FAMILY_NONLINEAR;
-  static_assert(!SCH || (NL && !GEN::HAS_S), "the workgroup SCHUR path is the nonlinear family's (dH/dy = 0)");
-  __shared__ SolveShared<NVMAX, NSMAX> S;
+  // QP SCHUR (gj_vr.hpp): the Schur complement on the matrix cores, blocked Gauss-Jordan
+  constexpr bool QPS = SCH && FAMILY == MCPX_FAMILY_QP;
+  constexpr bool NLS = SCH && NL;  // the nonlinear family's SCHUR (generated tables; GEN's null tables otherwise)
+  static_assert(!SCH || QPS || (NL && !GEN::HAS_S), "the workgroup SCHUR path: QP, or the nonlinear family's dH/dy = 0");
+  static_assert(!QPS || kVr<NSMAX>, "the QP SCHUR step is register-resident");
+  __shared__ SolveShared<NVMAX, NSMAX, kVr<NSMAX>, QPS> S;
+  // QP SCHUR: D⁻¹, 1 / w, ry, ty per constraint and rr per row, in LDS
+  __shared__ double qd[QPS ? NVMAX / 2 : 1], qw[QPS ? NVMAX / 2 : 1], qy[QPS ? NVMAX / 2 : 1],
+      qt[QPS ? NVMAX / 2 : 1], qr[QPS ? NSMAX : 1];
   const KernelArgs& a = W.k;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = a.n, m = a.m, N = n + 2 * m;
@@ -555,7 +577,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
   double* const zs = S.zs;
   double* const Fs = S.Fs;
   double* const dzs = S.dzs;
-  __shared__ double sv[SCH && kVr<NSMAX> ? 64 * GEN::SE_ER : 1];  // VR SCHUR: the sparse entries of [S | rr]
+  __shared__ double sv[NLS && kVr<NSMAX> ? 64 * GEN::SE_ER : 1];  // VR SCHUR: the sparse entries of [S | rr]
 
   for (;;) {
     if (tid == 0) S.sc.inst = atomicAdd(W.counter, 1);  // the work queue
@@ -579,6 +601,17 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
       if (tid == 0) GEN::init(th, blk);
     }
     __syncthreads();
+    // QP SCHUR: M exactly symmetric ⇒ S symmetric ⇒ the pivot-free Gauss-Jordan first (the
+    // oracle's m_sym), else the pivoting LU at every step.  Once per instance.
+    bool msym = false;
+    if constexpr (QPS) {
+      uint64_t asym = 0;
+      for (int q = tid; q < n * n; q += WG) {
+        const int j = q / n, i = q - j * n;
+        asym |= !(th[(int64_t)j * n + i] == th[(int64_t)i * n + j]);
+      }
+      msym = wg_or(asym, S.sc) == 0;
+    }
 
     double eps = 1.0;                   // :67
     double kkt = __builtin_huge_val();  // :68
@@ -596,6 +629,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
           __syncthreads();
         }
         double mx = 0.0;
+        for (int rep = 0; rep < (MCPX_WG_TWICE == 2 ? 2 : 1); ++rep)
         for (int i = tid; i < N; i += WG) {
           const double f = residual<FAMILY, GEN>(th, blk, zs, n, m, eps, i);
           Fs[i] = f;
@@ -603,7 +637,26 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
         }
         const double kkt_step = wg_max_nan(mx, S.sc);  // ‖F‖∞ (:107), committed after the step
         // ---- the Newton system (:81-83) as [K | rhs] -------------------------------
-        if constexpr (SCH) {
+        if constexpr (QPS) {  // the oracle's SCHUR branch (solve_one), QP family
+          for (int k = tid; k < m; k += WG) {
+            const double rw = 1.0 / (zs[n + k] + tol);  // 1 / J[c][c], J[c][c] = y_k + tol
+            const double D = (0.0 + tol) + zs[n + m + k] * rw;
+            const double Di = 1.0 / D;
+            const double ry = (-Fs[n + k]) - (Fs[n + m + k] * rw);
+            qd[k] = Di;
+            qw[k] = rw;
+            qy[k] = ry;
+            qt[k] = ry * Di;
+          }
+          __syncthreads();
+          const double* __restrict__ tA = th + (int64_t)n * n;
+          for (int i = tid; i < n; i += WG) {  // rr_i = −F_Gi + Σ_k A_ki ty_k
+            double acc = -Fs[i];
+            for (int k = 0; k < m; ++k) acc = fma(tA[(int64_t)i * m + k], qt[k], acc);
+            qr[i] = acc;
+          }
+          __syncthreads();
+        } else if constexpr (SCH) {
           // eliminate δs_k (pivot w_k = y_k + tol), then δy_k (pivot D_k = (0 + tol) + s_k / w_k)
           for (int k = tid; k < m; k += WG) {
             const double rw = 1.0 / (zs[n + k] + tol);
@@ -620,7 +673,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
         // VR SCHUR: the entries of [S | rr] beyond P + tol·I and −F_G (the generated
         // mcpx_nl_se_* tables: 360 at T = 10), each with its fma chain, once per step into
         // LDS; the LU's staging writes them over the dense part (`patch`)
-        if constexpr (SCH && kVr<NSMAX>) {
+        if constexpr (NLS && kVr<NSMAX>) {
           const int32_t* sp = GEN::se_pos();
           const int32_t* sk = GEN::se_k();
           for (int e = tid; e < 64 * GEN::SE_ER; e += WG) {
@@ -645,7 +698,7 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
         // and rr_i = −F_Gi + Σ_{k ∈ K(i)} (−Q_ik) ty_k; otherwise ∇F_z + tol·I (RED: with
         // the slack block eliminated) and −F.
         auto entry = [&](int i, int j) -> double {
-          if constexpr (SCH && kVr<NSMAX>) {  // the dense part; sv patches the rest
+          if constexpr (NLS && kVr<NSMAX>) {  // the dense part; sv patches the rest
             if (j < n) return i == j ? blk[GEN::OFF_P + j * n + i] + tol : blk[GEN::OFF_P + j * n + i];
             return -Fs[i];
           } else if constexpr (SCH) {
@@ -690,10 +743,36 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
         // generated nonlinear modules' SCHUR step: reciprocal multipliers (oracle lu_solve_x)
         constexpr bool RCP = FAMILY == MCPX_FAMILY_NONLINEAR && SOLVER == MCPX_LINSOLVE_SCHUR;
         bool lu_ok;
-        if constexpr (kVr<NSMAX> && SCH) {  // entries straight into registers (lu_vr.hpp)
+        if constexpr (QPS) {
+          bool gj_ok = false;
+          if (msym) {
+            d4 acc[GjDims<NSMAX>::TPW];
+            gj_form<NSMAX>(acc, th, n, m, tol, qd, qr);
+            gj_ok = gj_solve<NSMAX>(acc, n, dzs, S.lu.gj);
+          }
+          lu_ok = true;
+          if (!gj_ok) {  // the oracle's lu_solve of S (recomputed: the tiles were overwritten)
+            __syncthreads();
+            const int m4 = (m + 3) & ~3;
+            const double* __restrict__ tA = th + (int64_t)n * n;
+            auto sentry = [&](int i, int j) -> double {
+              if (j == n) return qr[i];
+              double acc = th[(int64_t)j * n + i];
+              if (i == j) acc += tol;
+              for (int k = 0; k < m4; ++k)
+                acc = k < m ? fma(tA[(int64_t)i * m + k], tA[(int64_t)j * m + k] * qd[k], acc) : fma(0.0, 0.0, acc);
+              return acc;
+            };
+            lu_ok = lu_solve_vr<NSMAX, 1, false>(sentry, n, dzs, S.lu.vr);
+          }
+        } else if constexpr (kVr<NSMAX> && SCH) {  // entries straight into registers (lu_vr.hpp)
           lu_ok = lu_solve_vr<NSMAX, 1, RCP>(entry, ns, dzs, S.lu, 1, nullptr, SePatch<GEN>{sv, n});
         } else if constexpr (kVr<NSMAX>) {
           lu_ok = lu_solve_vr<NSMAX, 1, RCP>(entry, ns, dzs, S.lu);
+          if (MCPX_WG_TWICE == 1) {
+            __syncthreads();
+            lu_ok = lu_solve_vr<NSMAX, 1, RCP>(entry, ns, dzs, S.lu);
+          }
         } else {  // [K | rhs] into the slot's workspace, then the HBM LU
           for (int i = wave; i < ns; i += NWAVE)
             for (int j = lane; j <= ns; j += 64) Am[(int64_t)i * ld + j] = entry(i, j);  // wave per row
@@ -705,7 +784,16 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
           reason |= MCPX_FAIL_LINSOLVE;
           break;
         }
-        if constexpr (SCH) {  // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
+        if constexpr (QPS) {  // δy_k = (ry_k − Σ_j A_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
+          const double* __restrict__ tA = th + (int64_t)n * n;
+          for (int k = tid; k < m; k += WG) {
+            double acc = qy[k];
+            for (int j = 0; j < n; ++j) acc = fma(-tA[(int64_t)j * m + k], dzs[j], acc);
+            const double dy = acc * qd[k];
+            dzs[n + k] = dy;
+            dzs[n + m + k] = fma(-zs[n + m + k], dy, -Fs[n + m + k]) * qw[k];
+          }
+        } else if constexpr (SCH) {  // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
           const int32_t* rp = GEN::rj_ptr();
           const int32_t* ri = GEN::rj_idx();
           for (int k = tid; k < m; k += WG) {

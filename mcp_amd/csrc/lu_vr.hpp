@@ -20,6 +20,13 @@
 // doubles per lane (VGPRs and AGPRs; one workgroup per CU).
 #pragma once
 
+// MCPX_VR_TWICE (diagnostic builds only, tools/ab_build.py): one phase of lu_solve_vr runs twice
+// — 1 the staging of [K | rhs] into the tiles, 2 the back substitution.  Both are idempotent, so
+// the bits stay the product's and the time added is the phase's cost.
+#ifndef MCPX_VR_TWICE
+#define MCPX_VR_TWICE 0
+#endif
+
 namespace mcpx {
 namespace wg {
 
@@ -118,6 +125,7 @@ __device__ __forceinline__ bool lu_solve_vr(const Entry& entry, int ns, double* 
   const int ncols = ns + nrhs;
   d4 acc[TPW];
   // ---- [K | rhs] into the tiles, one column tile at a time through the panel buffer --
+  for (int rep = 0; rep < (MCPX_VR_TWICE == 1 ? 2 : 1); ++rep)
   for (int tc = 0; tc < T; ++tc) {
     if (16 * tc >= ncols) break;  // uniform
     for (int q = tid; q < ns * 16; q += WG) {  // column-major: consecutive threads, consecutive rows
@@ -274,6 +282,7 @@ __device__ __forceinline__ bool lu_solve_vr(const Entry& entry, int ns, double* 
   }
   // ---- back substitution, blocked by 16 columns (oracle order: row i takes
   //      fma(−u_ik, x_k, b_i) for k = ns−1 down to step_of(i)+1) -----------------------
+  for (int rep = 0; rep < (MCPX_VR_TWICE == 2 ? 2 : 1); ++rep)
   for (int rc = 0; rc < nrhs; ++rc) {
     const int cb = ns + rc;
 #pragma unroll

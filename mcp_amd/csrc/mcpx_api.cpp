@@ -159,7 +159,9 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
     const int N = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : (ls == MCPX_LINSOLVE_REDUCED ? d->n + d->m : d->n);
     const int lanes = ls == MCPX_LINSOLVE_DENSE ? d->n + 2 * d->m : d->n + d->m;  // one wave: one lane per row
     wave_ok = pick_nmax(N) > 0 && lanes <= MCPX_MAX_KKT_DIM;
-    wg_ok = ls != MCPX_LINSOLVE_SCHUR && d->n + 2 * d->m <= MCPX_MAX_WG_KKT_DIM;
+    // workgroup kernels: REDUCED / DENSE, and SCHUR for the QP family up to n = 128 (gj_vr.hpp)
+    wg_ok = (ls != MCPX_LINSOLVE_SCHUR || (d->family == MCPX_FAMILY_QP && d->n <= mcpx::wg::kGjMax)) &&
+            d->n + 2 * d->m <= MCPX_MAX_WG_KKT_DIM;
     *nmax = wave_ok && p->kernel != MCPX_KERNEL_WORKGROUP ? pick_nmax(N) : pick_wg_bucket(d->n + 2 * d->m);
   }
   if (p->kernel == MCPX_KERNEL_WAVE) wg_ok = false;
@@ -171,8 +173,9 @@ int prepare(const mcpx_desc* d, const mcpx_params* p, mcpx::KernelArgs* a, int* 
                   p->kernel == MCPX_KERNEL_WAVE ? "one-wave" : (p->kernel == MCPX_KERNEL_WORKGROUP ? "workgroup" : ""),
                   ls, d->n, d->m);
     return fail(MCPX_EUNSUPPORTED, "problem size n=%d m=%d, linear_solver=%d exceeds the kernels (one wave: "
-                "reduced/schur n+m <= %d, dense n+2m <= %d; workgroup: reduced/dense n+2m <= %d, no schur)",
-                d->n, d->m, ls, MCPX_MAX_KKT_DIM, MCPX_MAX_KKT_DIM, MCPX_MAX_WG_KKT_DIM);
+                "reduced/schur n+m <= %d, dense n+2m <= %d; workgroup: reduced/dense n+2m <= %d, "
+                "schur: QP family, n <= %d)",
+                d->n, d->m, ls, MCPX_MAX_KKT_DIM, MCPX_MAX_KKT_DIM, MCPX_MAX_WG_KKT_DIM, mcpx::wg::kGjMax);
   }
   *wg = !wave_ok;
   if (!(p->tol > 0) || !(p->min_stepsize > 0) || !(p->decay > 0 && p->decay < 1) || std::isnan(p->tau) ||

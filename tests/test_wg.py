@@ -70,7 +70,8 @@ def test_kernel_selection_errors_before_any_device_work():
     assert _host_call(4, 2, kernel=7) == _abi.MCPX_EINVAL
     assert _host_call(300, 200, linear_solver="dense", kernel="wave") == _abi.MCPX_EUNSUPPORTED  # N = 700 > 64
     assert _host_call(300, 300, linear_solver="dense") == _abi.MCPX_EUNSUPPORTED  # N = 900 > 768
-    assert _host_call(100, 20, linear_solver="schur") == _abi.MCPX_EUNSUPPORTED  # no QP schur beyond one wave
+    assert _host_call(130, 20, linear_solver="schur") == _abi.MCPX_EUNSUPPORTED  # QP schur: n ≤ 128
+    assert _host_call(100, 20, family=1, linear_solver="schur") == _abi.MCPX_EUNSUPPORTED  # affine: one wave only
 
 
 def test_default_params_select_auto():
@@ -119,6 +120,57 @@ def test_large_qp_vs_oracle(gpu, oracle_lib, n, m, ls, B):
     got = solve_batch(0, n, m, th, tol=1e-6, linear_solver=ls, trace_len=TRACE)
     assert np.all(got["status"] == 0)
     assert_bit_exact(got, ref)
+
+
+def _indefinite(th, n, m, scale):
+    """M ← M − scale·I: symmetric, so the Gauss-Jordan is tried, but S loses positive definiteness
+    on some Newton steps (a pivot ≤ 0: the step falls back to the pivoting LU, as the oracle)."""
+    th = th.copy()
+    idx = np.arange(n) * (n + 1)
+    th[:, idx] -= scale
+    return th
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,B,case", [(128, 64, 48, "spd"), (100, 37, 32, "spd"), (70, 10, 32, "spd"),
+                                        (33, 40, 32, "spd"), (128, 64, 8, "asym"), (60, 20, 16, "indef"),
+                                        (128, 64, 8, "sparse")])
+def test_qp_schur_workgroup_vs_oracle(gpu, oracle_lib, n, m, B, case):
+    """The QP family's workgroup SCHUR step (csrc/gj_vr.hpp: the Schur complement on the matrix
+    cores, blocked Gauss-Jordan with MFMA trailing updates) beyond the one-wave kernel's
+    n + m ≤ 64: bit-exact against the oracle's SCHUR step (solve_one: S with the MFMA K padding,
+    gj_spd_solve) — ragged n and m (panels and K-chunks not multiples of 16 / 4), M not symmetric
+    (the pivoting LU at every step), M − c·I (pivots ≤ 0 on some steps: the LU fallback), sparse
+    QPs (failing instances, 931 Newton steps)."""
+    from mcp_amd.batch import solve_batch
+
+    sp = 0.9 if case == "sparse" else 0.0
+    th = generate_random_parameter(np.random.default_rng(n * 7 + m), n, m, sp, batch=B)
+    if case == "asym":
+        th[:, 1] += 1e-3  # M_21 ≠ M_12
+    if case == "indef":
+        th = _indefinite(th, n, m, 3.0)
+    ref = oracle_lib.solve_batch(0, n, m, th, tol=1e-6, linear_solver="schur", trace_len=TRACE, nthreads=8)
+    got = solve_batch(0, n, m, th, tol=1e-6, linear_solver="schur", trace_len=TRACE)
+    assert_bit_exact(got, ref)
+    if case in ("spd", "asym"):
+        assert np.all(ref["status"] == 0)
+
+
+@pytest.mark.gpu
+def test_qp_schur_workgroup_forced_equals_one_wave(gpu, oracle_lib):
+    """A size the one-wave SCHUR kernel solves (n = 32, m = 16), forced onto the workgroup SCHUR
+    kernel: the same bits as the one-wave kernel and the oracle (the two kernels' Gauss-Jordan
+    eliminations are the same chains)."""
+    from mcp_amd.batch import solve_batch
+
+    n, m, B = 32, 16, 64
+    th = generate_random_parameter(np.random.default_rng(9), n, m, 0.0, batch=B)
+    ref = oracle_lib.solve_batch(0, n, m, th, tol=1e-6, linear_solver="schur", trace_len=TRACE, nthreads=8)
+    got = solve_batch(0, n, m, th, tol=1e-6, linear_solver="schur", trace_len=TRACE, kernel="workgroup")
+    assert_bit_exact(got, ref)
+    wave = solve_batch(0, n, m, th, tol=1e-6, linear_solver="schur", trace_len=TRACE, kernel="wave")
+    assert_bit_exact(got, wave)
 
 
 @pytest.mark.gpu
