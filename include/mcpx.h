@@ -139,7 +139,10 @@ extern "C" {
  *                         takes the same branch (gj_spd_solve / lu_solve); a QP
  *                         passed as affine (P = M, Q = −Aᵀ, R = A, g = −ϕ, h = −b)
  *                         gives the QP solve's bits.  Modules: dense LU with
- *                         partial pivoting.  One wave: n + m ≤ 64. */
+ *                         partial pivoting.  One wave: n + m ≤ 64; the QP family
+ *                         also on one workgroup per instance up to n = 128 (S formed
+ *                         on MFMA, blocked Gauss-Jordan with MFMA trailing updates,
+ *                         the same bits). */
 #define MCPX_LINSOLVE_REDUCED 0
 #define MCPX_LINSOLVE_DENSE 1
 #define MCPX_LINSOLVE_SCHUR 2

@@ -29,8 +29,32 @@
 //   solution   x_i = b_i / S_ii (gj_spd_solve's final division by the step-i pivot).
 #pragma once
 
+// MCPX_GJ_STAMPS (diagnostic builds only, tools/gj_phase.hip): thread 0 of each workgroup adds
+// s_memtime cycles per phase into gj_stamp_acc[block][phase] — 0 panel staging, 1 the pivot
+// block (one wave), 2 the other rows' multipliers and the pivot rows' chains, 3 the MFMA
+// trailing update, 4 the solution, 5 the formation of S.
+#ifndef MCPX_GJ_STAMPS
+#define MCPX_GJ_STAMPS 0
+#endif
+
 namespace mcpx {
 namespace wg {
+
+#if MCPX_GJ_STAMPS
+__device__ uint64_t gj_stamp_acc[2048 * 8];
+#define GJ_STAMP(i)                                                 \
+  do {                                                              \
+    if (threadIdx.x == 0) {                                         \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
+      gj_stamp_acc[blockIdx.x * 8 + (i)] += t_ - gj_t0;             \
+      gj_t0 = t_;                                                   \
+    }                                                               \
+  } while (0)
+#else
+#define GJ_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 // The wave index, opaque to the optimiser (recomputed per tile, as lu_vr.hpp's vr_opaque) and
 // uniform by readfirstlane.  (vr_opaque's "+s" constraint here, next to the LU fallback,
@@ -63,15 +87,18 @@ struct GjShared {
 
 // C ← M + tol·I, then Σ_k A_ki (A_kj·D_k⁻¹) on the MFMA; column n = rr (LDS); the rest 0.
 // th: the instance's θ (QP layout: M n×n column-major, then A m×n column-major).
+// tA: the A block (m × n column-major) — θ's, or the instance's copy in LDS when it fits.
 template <int NSMAX>
-__device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const double* __restrict__ th, int n, int m,
-                                        double tol, const double* Di, const double* rr) {
+__device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const double* __restrict__ th,
+                                        const double* __restrict__ tA, int n, int m, double tol, const double* Di,
+                                        const double* rr) {
   using D = GjDims<NSMAX>;
   constexpr int R = D::R;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m4 = (m + 3) & ~3;
-  const double* __restrict__ tA = th + (int64_t)n * n;
+  uint64_t gj_t0 = MCPX_GJ_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+  (void)gj_t0;
 #pragma unroll
   for (int u = 0; u < D::TPW; ++u) {
     __builtin_amdgcn_sched_barrier(0);  // one tile at a time
@@ -94,6 +121,7 @@ __device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const dou
       const bool oka = ra < n, okb = col < n;
       const double* pa = tA + (int64_t)(oka ? ra : 0) * m;
       const double* pb = tA + (int64_t)(okb ? col : 0) * m;
+#pragma unroll 4
       for (int q = 0; q < m4; q += 4) {
         const int k = q + lr;
         const bool in = k < m;
@@ -110,6 +138,7 @@ __device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const dou
     }
     acc[u] = c;
   }
+  GJ_STAMP(5);
 }
 
 // gj_spd_solve on the tiles: x (LDS, ≥ n) = S⁻¹ rr.  False: a pivot that is not > 0 (the
@@ -122,6 +151,8 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid == 0) L.fail = 0;
+  uint64_t gj_t0 = MCPX_GJ_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
+  (void)gj_t0;
   for (int k0 = 0; k0 < n; k0 += 16) {
     const int tc = k0 >> 4, kb = min(16, n - k0), j_lo = k0 + kb;
     // ---- the panel (columns k0 .. k0+kb−1 of every row) and the pivot rows' trailing
@@ -142,6 +173,7 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
       }
     }
     __syncthreads();
+    GJ_STAMP(0);
     // ---- 1. the pivot rows' block, one wave, lane = block row ----------------------------
     if (wave == 0) {
       double pr[16];
@@ -151,12 +183,15 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk) {
         if (kk >= kb) continue;  // uniform
-        const double piv = __shfl(pr[kk], kk, 64);
+        const double piv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pr[kk]), kk),
+                                            __builtin_amdgcn_readlane(__double2loint(pr[kk]), kk));
         bad |= !(piv > 0.0);
         const double rp = 1.0 / piv;
         double u[16];
 #pragma unroll
-        for (int jj = kk + 1; jj < 16; ++jj) u[jj] = __shfl(pr[jj], kk, 64);
+        for (int jj = kk + 1; jj < 16; ++jj)
+          u[jj] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pr[jj]), kk),
+                                   __builtin_amdgcn_readlane(__double2loint(pr[jj]), kk));
         if (lane == kk) {
 #pragma unroll
           for (int jj = kk + 1; jj < 16; ++jj) pr[jj] = fma(pr[jj], 0.0, pr[jj]);
@@ -177,6 +212,7 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
       if (bad && lane == 0) L.fail = 1;
     }
     __syncthreads();
+    GJ_STAMP(1);
     // uniform by construction (readfirstlane): an LDS value as the branch condition made the
     // rest of the elimination divergent, and the tiles' uniform indices illegal VGPR→SGPR copies
     if (__builtin_amdgcn_readfirstlane(L.fail)) break;
@@ -218,6 +254,7 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
         if (r < kb) L.fb[r * UL + j] = v[r];
     }
     __syncthreads();
+    GJ_STAMP(2);
     // ---- 4. trailing update of every other row on the matrix cores; the pivot rows'
     //      final values into their tiles -------------------------------------------------
     const int kfull = kb & ~3;
@@ -240,12 +277,16 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
       const int ra = 16 * ti + lc;  // A-fragment row
       const bool oka = ra < n;
       d4 c = acc[u];
-      for (int q = 0; q < kfull; q += 4) {
-        const int kk = q + lr;
-        const double a = oka ? -L.pan[ra * PL + kk] : 0.0;
-        const double b = ctr ? L.u12[kk * UL + col] : 0.0;
-        c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+      double fa[4], fb[4];  // the fragments of all four K-chunks first: one LDS round trip
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kk = 4 * q + lr;
+        fa[q] = (oka && 4 * q < kfull) ? -L.pan[ra * PL + kk] : 0.0;
+        fb[q] = (ctr && 4 * q < kfull) ? L.u12[kk * UL + col] : 0.0;
       }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * q < kfull) c = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[q], fb[q], c, 0, 0, 0);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = 16 * ti + lr + 4 * e;
@@ -256,6 +297,7 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
       }
     }
     __syncthreads();
+    GJ_STAMP(3);
   }
   if (__builtin_amdgcn_readfirstlane(L.fail)) return false;
   // ---- x_i = b_i / S_ii -----------------------------------------------------------------
@@ -274,6 +316,7 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
   __syncthreads();
   for (int i = tid; i < n; i += WG) x[i] = L.xb[i] / L.piv[i];
   __syncthreads();
+  GJ_STAMP(4);
   return true;
 }
 

@@ -48,6 +48,15 @@ constexpr int kThreads = 256;       // workgroup size of every workgroup kernel 
 constexpr int kMaxDim = 768;        // largest system / vector dimension of the QP / affine kernels
 constexpr int kDimBuckets[4] = {128, 256, 512, 768};
 constexpr int kGjMax = 128;         // largest n of the QP family's workgroup SCHUR kernels (gj_vr.hpp)
+// doubles of the A block those kernels keep in LDS (m·n ≤ this): the largest m·n of bucket NV
+// (n ≤ 128, n + 2m ≤ NV), capped at 64 KB
+constexpr int kGjACapOf(int nv) {
+  int best = 1;
+  for (int n = 1; n <= kGjMax && n < nv; ++n) best = (n * ((nv - n) / 2) > best) ? n * ((nv - n) / 2) : best;
+  return best < 8192 ? best : 8192;
+}
+template <int NV>
+constexpr int kGjACap = kGjACapOf(NV);
 
 }  // namespace wg
 

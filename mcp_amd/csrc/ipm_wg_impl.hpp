@@ -502,8 +502,9 @@ __device__ __forceinline__ double jac(const double* __restrict__ th, const doubl
 }
 
 // MCPX_WG_TWICE (diagnostic builds only, tools/ab_build.py): 1 the register LU (lu_solve_vr)
-// of the QP / affine step runs twice, 2 the residual F — both idempotent (same bits, the added
-// time is the phase's cost).
+// of the QP / affine step runs twice, 2 the residual F; the QP SCHUR step (gj_vr.hpp): 3 the
+// formation and the Gauss-Jordan, 4 the formation, 5 rr, 6 δy and δs — all idempotent (same
+// bits, the added time is the phase's cost).
 #ifndef MCPX_WG_TWICE
 #define MCPX_WG_TWICE 0
 #endif
@@ -561,6 +562,9 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
   // QP SCHUR: D⁻¹, 1 / w, ry, ty per constraint and rr per row, in LDS
   __shared__ double qd[QPS ? NVMAX / 2 : 1], qw[QPS ? NVMAX / 2 : 1], qy[QPS ? NVMAX / 2 : 1],
       qt[QPS ? NVMAX / 2 : 1], qr[QPS ? NSMAX : 1];
+  // QP SCHUR: the instance's A block in LDS when it fits (every Newton step reads it five times:
+  // the residual's H rows aside, rr, the Schur complement's two fragments, δy)
+  __shared__ double sA[QPS ? kGjACap<NVMAX> : 1];
   const KernelArgs& a = W.k;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = a.n, m = a.m, N = n + 2 * m;
@@ -603,8 +607,11 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
     __syncthreads();
     // QP SCHUR: M exactly symmetric ⇒ S symmetric ⇒ the pivot-free Gauss-Jordan first (the
     // oracle's m_sym), else the pivoting LU at every step.  Once per instance.
-    bool msym = false;
+    bool msym = false, a_lds = false;
     if constexpr (QPS) {
+      a_lds = n * m <= kGjACap<NVMAX>;
+      if (a_lds)
+        for (int q = tid; q < n * m; q += WG) sA[q] = th[(int64_t)n * n + q];
       uint64_t asym = 0;
       for (int q = tid; q < n * n; q += WG) {
         const int j = q / n, i = q - j * n;
@@ -649,11 +656,16 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
             qt[k] = ry * Di;
           }
           __syncthreads();
-          const double* __restrict__ tA = th + (int64_t)n * n;
-          for (int i = tid; i < n; i += WG) {  // rr_i = −F_Gi + Σ_k A_ki ty_k
-            double acc = -Fs[i];
-            for (int k = 0; k < m; ++k) acc = fma(tA[(int64_t)i * m + k], qt[k], acc);
-            qr[i] = acc;
+          auto rr = [&](const double* __restrict__ tA) {
+            for (int i = tid; i < n; i += WG) {  // rr_i = −F_Gi + Σ_k A_ki ty_k
+              double acc = -Fs[i];
+              for (int k = 0; k < m; ++k) acc = fma(tA[(int64_t)i * m + k], qt[k], acc);
+              qr[i] = acc;
+            }
+          };
+          for (int rep = 0; rep < (MCPX_WG_TWICE == 5 ? 2 : 1); ++rep) {
+            if (a_lds) rr(sA);
+            else rr(th + (int64_t)n * n);
           }
           __syncthreads();
         } else if constexpr (SCH) {
@@ -746,9 +758,14 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
         if constexpr (QPS) {
           bool gj_ok = false;
           if (msym) {
-            d4 acc[GjDims<NSMAX>::TPW];
-            gj_form<NSMAX>(acc, th, n, m, tol, qd, qr);
-            gj_ok = gj_solve<NSMAX>(acc, n, dzs, S.lu.gj);
+            for (int rep = 0; rep < (MCPX_WG_TWICE == 3 ? 2 : 1); ++rep) {
+              d4 acc[GjDims<NSMAX>::TPW];
+              for (int r2 = 0; r2 < (MCPX_WG_TWICE == 4 ? 2 : 1); ++r2) {
+                if (a_lds) gj_form<NSMAX>(acc, th, sA, n, m, tol, qd, qr);
+                else gj_form<NSMAX>(acc, th, th + (int64_t)n * n, n, m, tol, qd, qr);
+              }
+              gj_ok = gj_solve<NSMAX>(acc, n, dzs, S.lu.gj);
+            }
           }
           lu_ok = true;
           if (!gj_ok) {  // the oracle's lu_solve of S (recomputed: the tiles were overwritten)
@@ -785,13 +802,18 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
           break;
         }
         if constexpr (QPS) {  // δy_k = (ry_k − Σ_j A_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
-          const double* __restrict__ tA = th + (int64_t)n * n;
-          for (int k = tid; k < m; k += WG) {
-            double acc = qy[k];
-            for (int j = 0; j < n; ++j) acc = fma(-tA[(int64_t)j * m + k], dzs[j], acc);
-            const double dy = acc * qd[k];
-            dzs[n + k] = dy;
-            dzs[n + m + k] = fma(-zs[n + m + k], dy, -Fs[n + m + k]) * qw[k];
+          auto dyds = [&](const double* __restrict__ tA) {
+            for (int k = tid; k < m; k += WG) {
+              double acc = qy[k];
+              for (int j = 0; j < n; ++j) acc = fma(-tA[(int64_t)j * m + k], dzs[j], acc);
+              const double dy = acc * qd[k];
+              dzs[n + k] = dy;
+              dzs[n + m + k] = fma(-zs[n + m + k], dy, -Fs[n + m + k]) * qw[k];
+            }
+          };
+          for (int rep = 0; rep < (MCPX_WG_TWICE == 6 ? 2 : 1); ++rep) {
+            if (a_lds) dyds(sA);
+            else dyds(th + (int64_t)n * n);
           }
         } else if constexpr (SCH) {  // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
           const int32_t* rp = GEN::rj_ptr();

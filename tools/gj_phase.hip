@@ -1,0 +1,89 @@
+// Diagnostic build: per-phase cycles of the QP workgroup SCHUR step (csrc/gj_vr.hpp,
+// MCPX_GJ_STAMPS) on random QPs of the bench's distribution.  Not a timing build.
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -mllvm -amdgpu-mfma-vgpr-form=1 \
+//          -DMCPX_GJ_STAMPS=1 -I mcp_amd/csrc tools/gj_phase.hip -o tools/gj_phase
+// Run:   tools/gj_phase n m B
+#include "ipm_wg_impl.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+__global__ __launch_bounds__(mcpx::wg::kThreads) void gj_kernel(const mcpx::wg::WgArgs args) {
+  mcpx::wg::solve_instances<MCPX_FAMILY_QP, MCPX_LINSOLVE_SCHUR, 256, mcpx::wg::kGjMax, mcpx::wg::NoGen>(args);
+}
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 128, m = argc > 2 ? atoi(argv[2]) : 64;
+  const int B = argc > 3 ? atoi(argv[3]) : 512;
+  if (n > 128 || n + 2 * m > 256) { printf("n <= 128, n + 2m <= 256\n"); return 1; }
+  const int p = n * n + m * n + m + n;
+  std::mt19937_64 g(7);
+  std::normal_distribution<double> nd;
+  std::vector<double> th((size_t)B * p);
+  for (int b = 0; b < B; ++b) {
+    double* t = &th[(size_t)b * p];
+    std::vector<double> P(n * n);
+    for (auto& v : P) v = nd(g);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        double acc = 0;
+        for (int k = 0; k < n; ++k) acc += P[k * n + i] * P[k * n + j];
+        t[j * n + i] = acc;
+      }
+    for (int i = n * n; i < p; ++i) t[i] = nd(g);
+  }
+  double *dth, *x, *y, *s, *kkt, *eps, *work;
+  int *outer, *status, *newton, *counter;
+  (void)hipMalloc(&dth, th.size() * 8);
+  (void)hipMemcpy(dth, th.data(), th.size() * 8, hipMemcpyHostToDevice);
+  (void)hipMalloc(&x, (size_t)B * n * 8); (void)hipMalloc(&y, (size_t)B * m * 8); (void)hipMalloc(&s, (size_t)B * m * 8);
+  (void)hipMalloc(&kkt, B * 8); (void)hipMalloc(&eps, B * 8);
+  (void)hipMalloc(&outer, B * 4); (void)hipMalloc(&status, B * 4); (void)hipMalloc(&newton, B * 4);
+  (void)hipMalloc(&counter, 4); (void)hipMalloc(&work, 1 << 20);
+  mcpx::wg::WgArgs w;
+  std::memset((void*)&w, 0, sizeof w);
+  mcpx::KernelArgs& a = w.k;
+  a.theta = dth; a.theta_ld = p; a.x = x; a.y = y; a.s = s; a.kkt_error = kkt; a.eps = eps;
+  a.outer_iters = outer; a.status = status; a.newton_iters = newton;
+  a.n = n; a.m = m; a.family = MCPX_FAMILY_QP; a.solver = MCPX_LINSOLVE_SCHUR;
+  a.max_inner = 20; a.max_outer = 50; a.tol = 1e-6; a.decay = 0.5; a.c_tau = 1.0 - 0.995; a.n_trials = 15;
+  for (int k = 0; k <= 20; ++k) { a.tight[k] = 1 - exp(-0.1 * k); a.loose[k] = 1 + exp(-0.5 * k); }
+  w.work = work; w.counter = counter; w.batch = B; w.slot_stride = 0; w.ld = n + 1;
+  int cus = 0, per_cu = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gj_kernel, mcpx::wg::kThreads, 0);
+  const int grid = std::min(B, cus * std::max(per_cu, 1));
+  std::vector<uint64_t> zero(2048 * 8, 0);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  float ms = 0;
+  for (int rep = 0; rep < 2; ++rep) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(mcpx::wg::gj_stamp_acc), zero.data(), zero.size() * 8);
+    (void)hipMemset(counter, 0, 4);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(gj_kernel, dim3(grid), dim3(mcpx::wg::kThreads), 0, 0, w);
+    (void)hipEventRecord(e1);
+    if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
+    (void)hipEventElapsedTime(&ms, e0, e1);
+  }
+  std::vector<uint64_t> st(2048 * 8);
+  (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(mcpx::wg::gj_stamp_acc), st.size() * 8);
+  std::vector<int> nw(B), stv(B);
+  (void)hipMemcpy(nw.data(), newton, B * 4, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(stv.data(), status, B * 4, hipMemcpyDeviceToHost);
+  double tot[8] = {}, steps = 0;
+  int solved = 0;
+  for (int b = 0; b < grid; ++b)
+    for (int i = 0; i < 8; ++i) tot[i] += st[(size_t)b * 8 + i];
+  for (int b = 0; b < B; ++b) { steps += nw[b]; solved += stv[b] == 0; }
+  const char* nm[] = {"panel staging", "pivot block (1 wave)", "multipliers + pivot-row chains", "MFMA trailing update",
+                      "solution", "formation of S"};
+  printf("n=%d m=%d B=%d grid=%d (%d per CU): %.3f ms, %.1f Newton steps mean, %d solved; cycles per Newton step (s_memtime, wave 0):\n",
+         n, m, B, grid, per_cu, ms, steps / B, solved);
+  for (int i = 0; i < 6; ++i) printf("  %-32s %10.0f\n", nm[i], tot[i] / steps);
+  return 0;
+}
