@@ -29,6 +29,8 @@
 //   solution   x_i = b_i / S_ii (gj_spd_solve's final division by the step-i pivot).
 #pragma once
 
+#include <type_traits>
+
 // MCPX_GJ_STAMPS (diagnostic builds only, tools/gj_phase.hip): thread 0 of each workgroup adds
 // s_memtime cycles per phase into gj_stamp_acc[block][phase] — 0 panel staging, 1 the pivot
 // block (one wave), 2 the other rows' multipliers and the pivot rows' chains, 3 the MFMA
@@ -41,14 +43,16 @@ namespace mcpx {
 namespace wg {
 
 #if MCPX_GJ_STAMPS
-__device__ uint64_t gj_stamp_acc[2048 * 8];
-#define GJ_STAMP(i)                                                 \
-  do {                                                              \
-    if (threadIdx.x == 0) {                                         \
-      const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
-      gj_stamp_acc[blockIdx.x * 8 + (i)] += t_ - gj_t0;             \
-      gj_t0 = t_;                                                   \
-    }                                                               \
+// [block][wave][slot]: lane 0 of every wave; slots 0-5 the phases' work, 8-13 the barrier
+// waits that end them (GJ_WAIT)
+__device__ uint64_t gj_stamp_acc[2048 * 4 * 16];
+#define GJ_STAMP(i)                                                                      \
+  do {                                                                                   \
+    if ((threadIdx.x & 63) == 0) {                                                       \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();                                  \
+      gj_stamp_acc[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + (i)] += t_ - gj_t0;      \
+      gj_t0 = t_;                                                                        \
+    }                                                                                    \
   } while (0)
 #else
 #define GJ_STAMP(i) \
@@ -79,6 +83,7 @@ struct GjShared {
   double u12[16 * GjDims<NSMAX>::UL];      // pivot row s at its step s (B operand), trailing columns
   double fb[16 * GjDims<NSMAX>::UL];       // the pivot rows' trailing values (their tiles' source)
   double ud[16 * 16];                      // step 1's u_kj inside the panel (for step 2)
+  double lb[16 * 16];                      // the pivot rows' multipliers, [row][step] (0 at its own)
   double rp[NSMAX];                        // 1 / pivot per step
   double piv[NSMAX];                       // pivot per step (S_kk)
   double xb[NSMAX];                        // the final rhs column
@@ -104,37 +109,37 @@ __device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const dou
     __builtin_amdgcn_sched_barrier(0);  // one tile at a time
     const int t = gj_opaque(wave) + NWAVE * u, ti = t % R, tj = t / R;
     const int ln_ = vr_opaque_lane(lane), lr = ln_ >> 4, lc = ln_ & 15;
-    const int col = 16 * tj + lc;
+    // every lane loads from a clamped (valid) address and selects: a load behind a per-lane
+    // branch costs an EXEC-mask round trip per entry and waits the memory counter out
+    const int col = 16 * tj + lc, colc = min(col, n - 1);
     d4 c;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int row = 16 * ti + lr + 4 * e;
-      double v = 0.0;
-      if (row < n && col < n) {
-        v = th[(int64_t)col * n + row];  // M_ij = J[i][j]
-        if (row == col) v += tol;        // J[i][i] += tol
-      }
-      c[e] = v;
+      const int row = 16 * ti + lr + 4 * e, rowc = min(row, n - 1);
+      const double mv = th[(int64_t)colc * n + rowc];  // M_ij = J[i][j]
+      const double v = row == col ? mv + tol : mv;      // J[i][i] += tol
+      c[e] = (row < n && col < n) ? v : 0.0;
     }
     if (16 * ti < n && 16 * tj < n) {  // uniform: the tile holds S entries
       const int ra = 16 * ti + lc;      // A-fragment row (an S row)
       const bool oka = ra < n, okb = col < n;
-      const double* pa = tA + (int64_t)(oka ? ra : 0) * m;
-      const double* pb = tA + (int64_t)(okb ? col : 0) * m;
+      const double* pa = tA + (int64_t)min(ra, n - 1) * m;
+      const double* pb = tA + (int64_t)colc * m;
 #pragma unroll 4
       for (int q = 0; q < m4; q += 4) {
-        const int k = q + lr;
+        const int k = q + lr, kc = min(k, m - 1);
         const bool in = k < m;
-        const double a = (oka && in) ? pa[in ? k : 0] : 0.0;                // A_ki
-        const double b = (okb && in) ? pb[in ? k : 0] * Di[in ? k : 0] : 0.0;  // A_kj·D_k⁻¹
+        const double av = pa[kc], bv = pb[kc] * Di[kc];
+        const double a = (oka && in) ? av : 0.0;  // A_ki
+        const double b = (okb && in) ? bv : 0.0;  // A_kj·D_k⁻¹
         c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
       }
     }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {  // the rhs column and the padding (the MFMA's values there are discarded)
       const int row = 16 * ti + lr + 4 * e;
-      if (col == n) c[e] = row < n ? rr[row] : 0.0;
-      else if (col > n || row >= n) c[e] = 0.0;
+      const double r = rr[min(row, n - 1)];
+      c[e] = col == n ? (row < n ? r : 0.0) : ((col > n || row >= n) ? 0.0 : c[e]);
     }
     acc[u] = c;
   }
@@ -153,36 +158,44 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
   if (tid == 0) L.fail = 0;
   uint64_t gj_t0 = MCPX_GJ_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
   (void)gj_t0;
-  for (int k0 = 0; k0 < n; k0 += 16) {
-    const int tc = k0 >> 4, kb = min(16, n - k0), j_lo = k0 + kb;
-    // ---- the panel (columns k0 .. k0+kb−1 of every row) and the pivot rows' trailing
-    //      columns into LDS -------------------------------------------------------------
+  static_assert(NSMAX <= 128, "rows on threads 0-127, trailing columns on threads 128-255");
+  // one panel; KB = 16 (full panels: every width test folds) or 0 (the last, kb < 16)
+  auto panel = [&](const int k0, auto KBc) -> bool {
+    constexpr int KB = decltype(KBc)::value;
+    const int tc = k0 >> 4, kb = KB ? KB : min(16, n - k0), j_lo = k0 + kb;
+    // ---- the panel (columns k0 .. k0+15 of every row) and the pivot rows' trailing
+    //      columns into LDS (whole tiles: entries outside are never read) ------------------
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
       __builtin_amdgcn_sched_barrier(0);
       const int t = gj_opaque(wave) + NWAVE * u, ti = t % R, tj = t / R;
       const int ln_ = vr_opaque_lane(lane), lr = ln_ >> 4, lc = ln_ & 15;
       if (16 * ti >= n || 16 * tj > n || tj < tc) continue;  // uniform
-      const int col = 16 * tj + lc;
+      if (tj == tc) {  // uniform
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = 16 * ti + lr + 4 * e;
-        if (row >= n) continue;
-        if (tj == tc && lc < kb) L.pan[row * PL + lc] = acc[u][e];
-        if (ti == tc && col >= j_lo && col <= n) L.fb[(row - k0) * UL + col] = acc[u][e];
+        for (int e = 0; e < 4; ++e) L.pan[(16 * ti + lr + 4 * e) * PL + lc] = acc[u][e];
+      }
+      if (ti == tc) {  // uniform
+#pragma unroll
+        for (int e = 0; e < 4; ++e) L.fb[(lr + 4 * e) * UL + 16 * tj + lc] = acc[u][e];
       }
     }
-    __syncthreads();
     GJ_STAMP(0);
+    __syncthreads();
+    GJ_STAMP(8);
     // ---- 1. the pivot rows' block, one wave, lane = block row ----------------------------
     if (wave == 0) {
       double pr[16];
+      const int br = k0 + min(lane, 15);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) pr[q] = (lane < kb && q < kb) ? L.pan[(k0 + lane) * PL + q] : 0.0;
+      for (int q = 0; q < 16; ++q) {
+        const double v = L.pan[br * PL + q];
+        pr[q] = (KB || (lane < kb && q < kb)) ? v : 0.0;
+      }
       bool bad = false;
 #pragma unroll
       for (int kk = 0; kk < 16; ++kk) {
-        if (kk >= kb) continue;  // uniform
+        if (!KB && kk >= kb) continue;  // uniform
         const double piv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pr[kk]), kk),
                                             __builtin_amdgcn_readlane(__double2loint(pr[kk]), kk));
         bad |= !(piv > 0.0);
@@ -192,16 +205,12 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
         for (int jj = kk + 1; jj < 16; ++jj)
           u[jj] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pr[jj]), kk),
                                    __builtin_amdgcn_readlane(__double2loint(pr[jj]), kk));
-        if (lane == kk) {
+        // the pivot row: multiplier +0 (fma(a, 0, a)); the others: l = a_ik·(1/piv)
+        const bool me = lane == kk;
+        const double l = pr[kk] * rp;
 #pragma unroll
-          for (int jj = kk + 1; jj < 16; ++jj) pr[jj] = fma(pr[jj], 0.0, pr[jj]);
-          L.pan[(k0 + lane) * PL + kk] = 0.0;  // (the pivot row's own step: not a multiplier)
-        } else {
-          const double l = pr[kk] * rp;
-#pragma unroll
-          for (int jj = kk + 1; jj < 16; ++jj) pr[jj] = fma(-l, u[jj], pr[jj]);
-          if (lane < kb) L.pan[(k0 + lane) * PL + kk] = l;
-        }
+        for (int jj = kk + 1; jj < 16; ++jj) pr[jj] = me ? fma(pr[jj], 0.0, pr[jj]) : fma(-l, u[jj], pr[jj]);
+        if (lane < 16) L.lb[lane * 16 + kk] = me ? 0.0 : l;  // (lanes kb … 15: rows beyond, never read)
         if (lane == 0) {
 #pragma unroll
           for (int jj = kk + 1; jj < 16; ++jj) L.ud[kk * 16 + jj] = u[jj];
@@ -211,52 +220,58 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
       }
       if (bad && lane == 0) L.fail = 1;
     }
-    __syncthreads();
     GJ_STAMP(1);
+    __syncthreads();
+    GJ_STAMP(9);
     // uniform by construction (readfirstlane): an LDS value as the branch condition made the
     // rest of the elimination divergent, and the tiles' uniform indices illegal VGPR→SGPR copies
-    if (__builtin_amdgcn_readfirstlane(L.fail)) break;
-    // ---- 2. every other row: its multipliers (in place of its panel entries) ----------
-    {
+    if (__builtin_amdgcn_readfirstlane(L.fail)) return false;
+    if (tid < 128) {
+      // ---- 2. threads 0-127, row = thread: the other rows' multipliers (in place of their
+      //      panel entries: the MFMA's A fragments) ----------------------------------------
       const int row = tid;
       if (row < n && (row < k0 || row >= j_lo)) {
         double pr[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) pr[q] = q < kb ? L.pan[row * PL + q] : 0.0;
+        for (int q = 0; q < 16; ++q) pr[q] = L.pan[row * PL + q];
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) {
-          if (kk >= kb) continue;  // uniform
+          if (!KB && kk >= kb) continue;  // uniform
           const double l = pr[kk] * L.rp[k0 + kk];
 #pragma unroll
           for (int jj = kk + 1; jj < 16; ++jj)
-            if (jj < kb) pr[jj] = fma(-l, L.ud[kk * 16 + jj], pr[jj]);
+            if (KB || jj < kb) pr[jj] = fma(-l, L.ud[kk * 16 + jj], pr[jj]);
           L.pan[row * PL + kk] = l;
         }
       }
-    }
-    // ---- 3. thread = trailing column: the pivot rows' chains over the panel's steps ----
-    for (int j = j_lo + tid; j <= n; j += WG) {
-      double v[16];
+    } else {
+      // ---- 3. threads 128-255, trailing column = thread: the pivot rows' chains over the
+      //      panel's steps (each pivot row's value at its own step is U12, the B operand) ----
+      const int j = j_lo + (tid - 128);
+      if (j <= n) {
+        double v[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = r < kb ? L.fb[r * UL + j] : 0.0;
+        for (int r = 0; r < 16; ++r) v[r] = (KB || r < kb) ? L.fb[r * UL + j] : 0.0;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        if (s >= kb) continue;  // uniform
-        const double us = v[s];
-        L.u12[s * UL + j] = us;
-        v[s] = fma(us, 0.0, us);
+        for (int s = 0; s < 16; ++s) {
+          if (!KB && s >= kb) continue;  // uniform
+          const double us = v[s];
+          L.u12[s * UL + j] = us;
+          v[s] = fma(us, 0.0, us);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (r != s && (KB || r < kb)) v[r] = fma(-L.lb[r * 16 + s], us, v[r]);
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (r != s && r < kb) v[r] = fma(-L.pan[(k0 + r) * PL + s], us, v[r]);
+          if (KB || r < kb) L.fb[r * UL + j] = v[r];
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (r < kb) L.fb[r * UL + j] = v[r];
     }
-    __syncthreads();
     GJ_STAMP(2);
+    __syncthreads();
+    GJ_STAMP(10);
     // ---- 4. trailing update of every other row on the matrix cores; the pivot rows'
-    //      final values into their tiles -------------------------------------------------
+    //      final values into their tiles (per lane by selects, no per-lane branch) ----------
     const int kfull = kb & ~3;
 #pragma unroll
     for (int u = 0; u < TPW; ++u) {
@@ -270,7 +285,8 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = lr + 4 * e;
-          if (ctr && r < kb) acc[u][e] = L.fb[r * UL + col];
+          const double f = L.fb[r * UL + col];
+          acc[u][e] = (ctr && (KB || r < kb)) ? f : acc[u][e];
         }
         continue;
       }
@@ -281,25 +297,37 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int kk = 4 * q + lr;
-        fa[q] = (oka && 4 * q < kfull) ? -L.pan[ra * PL + kk] : 0.0;
-        fb[q] = (ctr && 4 * q < kfull) ? L.u12[kk * UL + col] : 0.0;
+        const double av = -L.pan[ra * PL + kk], bv = L.u12[kk * UL + col];
+        fa[q] = oka ? av : 0.0;
+        fb[q] = ctr ? bv : 0.0;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (4 * q < kfull) c = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[q], fb[q], c, 0, 0, 0);
+        if (KB || 4 * q < kfull) c = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[q], fb[q], c, 0, 0, 0);
+      if (!KB && kfull < kb) {  // uniform: a width not a multiple of 4, the rest on the VALU
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = min(16 * ti + lr + 4 * e, n - 1);
+          double v = c[e];
+          for (int kk = kfull; kk < kb; ++kk) v = fma(-L.pan[row * PL + kk], L.u12[kk * UL + col], v);
+          c[e] = v;
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = 16 * ti + lr + 4 * e;
-        if (row >= n || !ctr) continue;
-        double v = c[e];
-        for (int kk = kfull; kk < kb; ++kk) v = fma(-L.pan[row * PL + kk], L.u12[kk * UL + col], v);
-        acc[u][e] = v;
+        acc[u][e] = (row < n && ctr) ? c[e] : acc[u][e];
       }
     }
-    __syncthreads();
     GJ_STAMP(3);
-  }
-  if (__builtin_amdgcn_readfirstlane(L.fail)) return false;
+    __syncthreads();
+    GJ_STAMP(11);
+    return true;
+  };
+  bool ok = true;
+  for (int k0 = 0; k0 < n && ok; k0 += 16)
+    ok = n - k0 >= 16 ? panel(k0, std::integral_constant<int, 16>{}) : panel(k0, std::integral_constant<int, 0>{});
+  if (!ok) return false;
   // ---- x_i = b_i / S_ii -----------------------------------------------------------------
 #pragma unroll
   for (int u = 0; u < TPW; ++u) {

@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, gj_kernel, mcpx::wg::kThreads, 0);
   const int grid = std::min(B, cus * std::max(per_cu, 1));
-  std::vector<uint64_t> zero(2048 * 8, 0);
+  std::vector<uint64_t> zero(2048 * 4 * 16, 0);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   float ms = 0;
@@ -70,20 +70,28 @@ int main(int argc, char** argv) {
     if (hipDeviceSynchronize() != hipSuccess) { printf("kernel failed\n"); return 1; }
     (void)hipEventElapsedTime(&ms, e0, e1);
   }
-  std::vector<uint64_t> st(2048 * 8);
+  std::vector<uint64_t> st(zero.size());
   (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(mcpx::wg::gj_stamp_acc), st.size() * 8);
   std::vector<int> nw(B), stv(B);
   (void)hipMemcpy(nw.data(), newton, B * 4, hipMemcpyDeviceToHost);
   (void)hipMemcpy(stv.data(), status, B * 4, hipMemcpyDeviceToHost);
-  double tot[8] = {}, steps = 0;
+  double tot[4][16] = {}, steps = 0;
   int solved = 0;
   for (int b = 0; b < grid; ++b)
-    for (int i = 0; i < 8; ++i) tot[i] += st[(size_t)b * 8 + i];
+    for (int w4 = 0; w4 < 4; ++w4)
+      for (int i = 0; i < 16; ++i) tot[w4][i] += st[((size_t)b * 4 + w4) * 16 + i];
   for (int b = 0; b < B; ++b) { steps += nw[b]; solved += stv[b] == 0; }
   const char* nm[] = {"panel staging", "pivot block (1 wave)", "multipliers + pivot-row chains", "MFMA trailing update",
-                      "solution", "formation of S"};
-  printf("n=%d m=%d B=%d grid=%d (%d per CU): %.3f ms, %.1f Newton steps mean, %d solved; cycles per Newton step (s_memtime, wave 0):\n",
-         n, m, B, grid, per_cu, ms, steps / B, solved);
-  for (int i = 0; i < 6; ++i) printf("  %-32s %10.0f\n", nm[i], tot[i] / steps);
+                      "solution", "formation of S", "", "", "wait after staging", "wait after pivot block",
+                      "wait after multipliers/chains", "wait after trailing update"};
+  printf("n=%d m=%d B=%d grid=%d (%d per CU): %.3f ms, %.1f Newton steps mean, %d solved\n", n, m, B, grid, per_cu,
+         ms, steps / B, solved);
+  printf("s_memtime per Newton step, per wave:        wave0     wave1     wave2     wave3\n");
+  for (int i = 0; i < 12; ++i) {
+    if (!nm[i][0]) continue;
+    printf("  %-32s", nm[i]);
+    for (int w4 = 0; w4 < 4; ++w4) printf(" %9.0f", tot[w4][i] / steps);
+    printf("\n");
+  }
   return 0;
 }
