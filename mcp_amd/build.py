@@ -29,7 +29,7 @@ SOURCES = [os.path.join(CSRC, f) for f in (
     "ipm_inst_dense_qp.hip", "ipm_inst_dense_aff.hip", "sens_inst_vjp.hip", "sens_inst_jvp.hip",
     "ipm_inst_wg.hip", "ipm_inst_wg_vr.hip", "ipm_inst_wg_gj.hip", "sens_inst_wg.hip", "ipm_inst_fused.hip", "mcpx_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("ipm_kernel.h", "ipm_kernel_impl.hpp", "bcast_group.inc", "sens_kernel.h", "sens_kernel_impl.hpp",
-    "ipm_wg.h", "ipm_wg_impl.hpp", "lu_vr.hpp", "sens_wg_impl.hpp")] + [
+    "ipm_wg.h", "ipm_wg_impl.hpp", "lu_vr.hpp", "gj_vr.hpp", "sens_wg_impl.hpp")] + [
     os.path.join(ROOT, "include", "mcpx.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"

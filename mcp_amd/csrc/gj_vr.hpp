@@ -104,9 +104,23 @@ __device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const dou
   const int m4 = (m + 3) & ~3;
   uint64_t gj_t0 = MCPX_GJ_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
   (void)gj_t0;
+  // the tile's M entries (clamped addresses: every lane loads, the caller selects), one tile
+  // ahead: their global-memory latency hides behind the previous tile's MFMA chain
+  auto mload = [&](int u) {
+    const int t = gj_opaque(wave) + NWAVE * u, ti = t % R, tj = t / R;
+    const int ln_ = vr_opaque_lane(lane), lr = ln_ >> 4, lc = ln_ & 15;
+    const int colc = min(16 * tj + lc, n - 1);
+    d4 mv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) mv[e] = th[(int64_t)colc * n + min(16 * ti + lr + 4 * e, n - 1)];  // M_ij = J[i][j]
+    return mv;
+  };
+  d4 mnext = mload(0);
 #pragma unroll
   for (int u = 0; u < D::TPW; ++u) {
     __builtin_amdgcn_sched_barrier(0);  // one tile at a time
+    const d4 mcur = mnext;
+    if (u + 1 < D::TPW) mnext = mload(u + 1);
     const int t = gj_opaque(wave) + NWAVE * u, ti = t % R, tj = t / R;
     const int ln_ = vr_opaque_lane(lane), lr = ln_ >> 4, lc = ln_ & 15;
     // every lane loads from a clamped (valid) address and selects: a load behind a per-lane
@@ -115,9 +129,8 @@ __device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const dou
     d4 c;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int row = 16 * ti + lr + 4 * e, rowc = min(row, n - 1);
-      const double mv = th[(int64_t)colc * n + rowc];  // M_ij = J[i][j]
-      const double v = row == col ? mv + tol : mv;      // J[i][i] += tol
+      const int row = 16 * ti + lr + 4 * e;
+      const double v = row == col ? mcur[e] + tol : mcur[e];  // J[i][i] += tol
       c[e] = (row < n && col < n) ? v : 0.0;
     }
     if (16 * ti < n && 16 * tj < n) {  // uniform: the tile holds S entries
@@ -247,20 +260,30 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
     } else {
       // ---- 3. threads 128-255, trailing column = thread: the pivot rows' chains over the
       //      panel's steps (each pivot row's value at its own step is U12, the B operand) ----
-      const int j = j_lo + (tid - 128);
+      // columns interleaved over the two waves (the trailing set shrinks panel by panel)
+      const int q = tid - 128, j = j_lo + 2 * (q & 63) + (q >> 6);
       if (j <= n) {
         double v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = (KB || r < kb) ? L.fb[r * UL + j] : 0.0;
+        double lc[16], ln[16];  // step s's multipliers (column s of lb), the next step's loaded ahead
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lc[r] = L.lb[r * 16];
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
           if (!KB && s >= kb) continue;  // uniform
+          if (s + 1 < 16) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) ln[r] = L.lb[r * 16 + s + 1];
+          }
           const double us = v[s];
           L.u12[s * UL + j] = us;
           v[s] = fma(us, 0.0, us);
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            if (r != s && (KB || r < kb)) v[r] = fma(-L.lb[r * 16 + s], us, v[r]);
+            if (r != s && (KB || r < kb)) v[r] = fma(-lc[r], us, v[r]);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) lc[r] = ln[r];
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r)
