@@ -200,8 +200,9 @@ def test_unsupported_sizes(gpu, oracle_lib):
     th = generate_random_parameter(np.random.default_rng(0), 40, 30, 0.0, batch=2)
     with pytest.raises(MCPXError):
         solve_batch(0, 40, 30, th, kernel="wave")  # n + m = 70
-    with pytest.raises(MCPXError):
-        solve_batch(0, 40, 30, th, linear_solver="schur")
+    th130 = generate_random_parameter(np.random.default_rng(0), 130, 30, 0.0, batch=1)
+    with pytest.raises(MCPXError):  # QP SCHUR: one wave n + m ≤ 64, one workgroup n ≤ 128
+        solve_batch(0, 130, 30, th130, linear_solver="schur")
     th = generate_random_parameter(np.random.default_rng(0), 400, 200, 0.0, batch=1)
     with pytest.raises(MCPXError):
         solve_batch(0, 400, 200, th, linear_solver="dense")  # n + 2m = 800 > 768

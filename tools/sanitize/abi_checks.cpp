@@ -60,7 +60,7 @@ static void one_thread(int seed) {
   EXPECT(mcpx_solve_batch(&d, theta.data(), nullptr, nullptr, nullptr, &q, 1, &o) == MCPX_EUNSUPPORTED);
   q = p;
   q.linear_solver = MCPX_LINSOLVE_SCHUR;
-  mcpx_desc big{MCPX_FAMILY_QP, 100, 20, 0, 1, mcpx_theta_dim(MCPX_FAMILY_QP, 100, 20)};
+  mcpx_desc big{MCPX_FAMILY_QP, 130, 20, 0, 1, mcpx_theta_dim(MCPX_FAMILY_QP, 130, 20)};  // QP SCHUR: n ≤ 128
   EXPECT(mcpx_solve_batch(&big, theta.data(), nullptr, nullptr, nullptr, &q, 1, &o) == MCPX_EUNSUPPORTED);
   mcpx_out none{};
   EXPECT(mcpx_solve_batch(&d, theta.data(), nullptr, nullptr, nullptr, &p, 1, &none) == MCPX_EINVAL);
