@@ -11,10 +11,14 @@
 //   formation  C ← M + tol·I (the oracle's J[i][i] += tol rounding), then per K-chunk of 4
 //              constraints v_mfma_f64_16x16x4_f64 with A-fragment A_ki and B-fragment
 //              A_kj·D_k⁻¹ (one rounding, as the oracle's akj·sD[k]); chunks past m are zeros,
-//              the oracle's fma(0, 0, acc) padding; rr on the VALU (no padding there).
+//              the oracle's fma(0, 0, acc) padding; rr on the VALU (no padding there).  A
+//              wave's two tiles of one column tile are formed together (one B fragment, two
+//              interleaved chains), four K-chunks' LDS reads ahead of their MFMAs; the A copy in
+//              LDS has an odd row stride (kGjLda) so a fragment's 16 rows hit 16 banks.
 //   panel k0   (16 columns; every row of S takes every step's update in Gauss-Jordan):
 //              1. the 16 pivot rows' panel block (rows k0 .. k0+15) is eliminated by one
-//                 wave, lane = row: per step the pivot (pivot-free: S SPD, row k at step k;
+//                 wave, lane = row (the pivot row reaches the fmas as a DPP row_newbcast
+//                 operand): per step the pivot (pivot-free: S SPD, row k at step k;
 //                 a pivot ≤ 0 or NaN abandons the elimination), one correctly rounded
 //                 reciprocal, l = a_ik·(1/piv), a_ij ← fma(−l, u_kj, a_ij), the pivot row
 //                 itself fma(a, 0, a) (gj_spd_solve's multiplier +0 update);
@@ -37,6 +41,11 @@
 // trailing update, 4 the solution, 5 the formation of S.
 #ifndef MCPX_GJ_STAMPS
 #define MCPX_GJ_STAMPS 0
+#endif
+// MCPX_GJ_FORM_PAIR: the formation takes a wave's two tiles of one column tile together (they
+// share the B fragment; two independent MFMA chains).  0: one tile at a time.
+#ifndef MCPX_GJ_FORM_PAIR
+#define MCPX_GJ_FORM_PAIR 1
 #endif
 
 namespace mcpx {
@@ -68,6 +77,34 @@ __device__ __forceinline__ int gj_opaque(int v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+template <int K, int E, class F>
+__device__ __forceinline__ void gj_static_for(F&& f) {
+  if constexpr (K < E) {
+    f(std::integral_constant<int, K>{});
+    gj_static_for<K + 1, E>(f);
+  }
+}
+
+// acc ← fma(nl, u, acc) with u = lane R of acc's 16-lane row (v_fmac_f64_dpp row_newbcast:R; the
+// DPP read precedes the write, so every lane sees lane R's old value).  s_nop 1: the two wait
+// states a VALU write needs before a DPP read of the same register, whatever the compiler
+// placed just ahead of the asm.
+#define GJ_FMAC_NB(R)                                                                                 \
+  case R:                                                                                             \
+    asm volatile("s_nop 1\n v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf" \
+                 : "+v"(acc)                                                                          \
+                 : "v"(nl));                                                                          \
+    break;
+template <int R>
+__device__ __forceinline__ void gj_fmac_bcast_self(double& acc, double nl) {
+  switch (R) {
+    GJ_FMAC_NB(0) GJ_FMAC_NB(1) GJ_FMAC_NB(2) GJ_FMAC_NB(3) GJ_FMAC_NB(4) GJ_FMAC_NB(5) GJ_FMAC_NB(6)
+    GJ_FMAC_NB(7) GJ_FMAC_NB(8) GJ_FMAC_NB(9) GJ_FMAC_NB(10) GJ_FMAC_NB(11) GJ_FMAC_NB(12) GJ_FMAC_NB(13)
+    GJ_FMAC_NB(14) GJ_FMAC_NB(15)
+  }
+}
+#undef GJ_FMAC_NB
+
 template <int NSMAX>
 struct GjDims {
   static constexpr int R = (NSMAX + 15) / 16;           // row tiles
@@ -92,10 +129,11 @@ struct GjShared {
 
 // C ← M + tol·I, then Σ_k A_ki (A_kj·D_k⁻¹) on the MFMA; column n = rr (LDS); the rest 0.
 // th: the instance's θ (QP layout: M n×n column-major, then A m×n column-major).
-// tA: the A block (m × n column-major) — θ's, or the instance's copy in LDS when it fits.
+// tA: the A block, row j of Aᵀ (column j of A) at tA[j·la] — θ's (la = m), or the instance's
+// copy in LDS when it fits (la = kGjLda(m)).
 template <int NSMAX>
 __device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const double* __restrict__ th,
-                                        const double* __restrict__ tA, int n, int m, double tol, const double* Di,
+                                        const double* __restrict__ tA, int la, int n, int m, double tol, const double* Di,
                                         const double* rr) {
   using D = GjDims<NSMAX>;
   constexpr int R = D::R;
@@ -115,6 +153,91 @@ __device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const dou
     for (int e = 0; e < 4; ++e) mv[e] = th[(int64_t)colc * n + min(16 * ti + lr + 4 * e, n - 1)];  // M_ij = J[i][j]
     return mv;
   };
+  if constexpr (MCPX_GJ_FORM_PAIR && R == 2 * NWAVE && D::TPW % 2 == 0) {
+    // Tiles 2v and 2v + 1 of a wave are row tiles `wave` and `wave` + 4 of column tile v: they
+    // share the B fragment A_kj·D_k⁻¹, so a K-chunk loads it once, and the two accumulators' MFMA
+    // chains interleave (each tile's chain is the same, in the same order: the same bits).
+    d4 mn0 = mload(0), mn1 = mload(1);
+#pragma unroll
+    for (int v = 0; v < D::TPW / 2; ++v) {
+      __builtin_amdgcn_sched_barrier(0);  // one column tile at a time
+      const d4 mc0 = mn0, mc1 = mn1;
+      if (2 * v + 2 < D::TPW) {
+        mn0 = mload(2 * v + 2);
+        mn1 = mload(2 * v + 3);
+      }
+      const int ti0 = gj_opaque(wave), ti1 = ti0 + NWAVE, tj = v;
+      const int ln_ = vr_opaque_lane(lane), lr = ln_ >> 4, lc = ln_ & 15;
+      const int col = 16 * tj + lc, colc = min(col, n - 1);
+      // uniform: both tiles inside S (no padding, not the rhs column) — the selects below are
+      // identities there except on the diagonal (behind a branch, the compiler sank the rhs
+      // column's LDS reads into divergent blocks that re-wrote the accumulators)
+      const bool inner = 16 * tj + 16 <= n && 16 * ti1 + 16 <= n;
+      d4 c0 = mc0, c1 = mc1;
+      if (!inner || ti0 == tj || ti1 == tj) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r0 = 16 * ti0 + lr + 4 * e, r1 = 16 * ti1 + lr + 4 * e;
+          const double v0 = r0 == col ? mc0[e] + tol : mc0[e], v1 = r1 == col ? mc1[e] + tol : mc1[e];
+          c0[e] = (r0 < n && col < n) ? v0 : 0.0;
+          c1[e] = (r1 < n && col < n) ? v1 : 0.0;
+        }
+      }
+      const bool okb = col < n;
+      const double* pb = tA + (int64_t)colc * la;
+      const int ra0 = 16 * ti0 + lc, ra1 = 16 * ti1 + lc;
+      const bool oka0 = ra0 < n, oka1 = ra1 < n;
+      const double* pa0 = tA + (int64_t)min(ra0, n - 1) * la;
+      const double* pa1 = tA + (int64_t)min(ra1, n - 1) * la;
+      if (16 * ti1 < n && 16 * tj < n) {  // uniform: both tiles hold S entries
+        // four K-chunks at a time, their 16 LDS reads issued ahead of the 8 MFMAs (the loop does
+        // not unroll at a run-time m, and a chunk that waited for its own reads serialised two
+        // LDS round trips with every MFMA pair); chunks past m4 only read (clamped addresses)
+        for (int q0 = 0; q0 < m4; q0 += 16) {
+          double gb[4], gd[4], g0[4], g1[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kc = min(q0 + 4 * j + lr, m - 1);
+            gb[j] = pb[kc];
+            gd[j] = Di[kc];
+            g0[j] = pa0[kc];
+            g1[j] = pa1[kc];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int q = q0 + 4 * j;
+            if (q < m4) {  // uniform
+              const bool in = q + lr < m;
+              const double b = (okb && in) ? gb[j] * gd[j] : 0.0;
+              c0 = __builtin_amdgcn_mfma_f64_16x16x4f64((oka0 && in) ? g0[j] : 0.0, b, c0, 0, 0, 0);
+              c1 = __builtin_amdgcn_mfma_f64_16x16x4f64((oka1 && in) ? g1[j] : 0.0, b, c1, 0, 0, 0);
+            }
+          }
+        }
+      } else if (16 * ti0 < n && 16 * tj < n) {  // the first only (n ≤ 16·(wave + 4))
+#pragma unroll 4
+        for (int q = 0; q < m4; q += 4) {
+          const int k = q + lr, kc = min(k, m - 1);
+          const bool in = k < m;
+          const double bv = pb[kc] * Di[kc], av0 = pa0[kc];
+          c0 = __builtin_amdgcn_mfma_f64_16x16x4f64((oka0 && in) ? av0 : 0.0, (okb && in) ? bv : 0.0, c0, 0, 0, 0);
+        }
+      }
+      if (!inner) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {  // the rhs column and the padding (as below)
+          const int r0 = 16 * ti0 + lr + 4 * e, r1 = 16 * ti1 + lr + 4 * e;
+          const double rv0 = rr[min(r0, n - 1)], rv1 = rr[min(r1, n - 1)];
+          c0[e] = col == n ? (r0 < n ? rv0 : 0.0) : ((col > n || r0 >= n) ? 0.0 : c0[e]);
+          c1[e] = col == n ? (r1 < n ? rv1 : 0.0) : ((col > n || r1 >= n) ? 0.0 : c1[e]);
+        }
+      }
+      acc[2 * v] = c0;
+      acc[2 * v + 1] = c1;
+    }
+    GJ_STAMP(5);
+    return;
+  }
   d4 mnext = mload(0);
 #pragma unroll
   for (int u = 0; u < D::TPW; ++u) {
@@ -136,8 +259,8 @@ __device__ __forceinline__ void gj_form(d4 (&acc)[GjDims<NSMAX>::TPW], const dou
     if (16 * ti < n && 16 * tj < n) {  // uniform: the tile holds S entries
       const int ra = 16 * ti + lc;      // A-fragment row (an S row)
       const bool oka = ra < n, okb = col < n;
-      const double* pa = tA + (int64_t)min(ra, n - 1) * m;
-      const double* pb = tA + (int64_t)colc * m;
+      const double* pa = tA + (int64_t)min(ra, n - 1) * la;
+      const double* pb = tA + (int64_t)colc * la;
 #pragma unroll 4
       for (int q = 0; q < m4; q += 4) {
         const int k = q + lr, kc = min(k, m - 1);
@@ -206,31 +329,30 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
         pr[q] = (KB || (lane < kb && q < kb)) ? v : 0.0;
       }
       bool bad = false;
-#pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        if (!KB && kk >= kb) continue;  // uniform
+      gj_static_for<0, 16>([&](auto KKc) {
+        constexpr int kk = decltype(KKc)::value;
+        if (!KB && kk >= kb) return;  // uniform
         const double piv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pr[kk]), kk),
                                             __builtin_amdgcn_readlane(__double2loint(pr[kk]), kk));
         bad |= !(piv > 0.0);
         const double rp = 1.0 / piv;
-        double u[16];
-#pragma unroll
-        for (int jj = kk + 1; jj < 16; ++jj)
-          u[jj] = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(pr[jj]), kk),
-                                   __builtin_amdgcn_readlane(__double2loint(pr[jj]), kk));
-        // the pivot row: multiplier +0 (fma(a, 0, a)); the others: l = a_ik·(1/piv)
         const bool me = lane == kk;
-        const double l = pr[kk] * rp;
+        if (me) {  // row kk at its step: U for step 2
 #pragma unroll
-        for (int jj = kk + 1; jj < 16; ++jj) pr[jj] = me ? fma(pr[jj], 0.0, pr[jj]) : fma(-l, u[jj], pr[jj]);
+          for (int jj = kk + 1; jj < 16; ++jj) L.ud[kk * 16 + jj] = pr[jj];
+        }
+        // the pivot row: multiplier +0 (fma(+0, a, a) = fma(a, 0, a)); the others: l = a_ik·(1/piv),
+        // a_ij ← fma(−l, u_kj, a_ij) with u_kj from lane kk by the fma's DPP operand
+        const double l = pr[kk] * rp;
+        const double nl = me ? 0.0 : -l;
+#pragma unroll
+        for (int jj = kk + 1; jj < 16; ++jj) gj_fmac_bcast_self<kk>(pr[jj], nl);
         if (lane < 16) L.lb[lane * 16 + kk] = me ? 0.0 : l;  // (lanes kb … 15: rows beyond, never read)
         if (lane == 0) {
-#pragma unroll
-          for (int jj = kk + 1; jj < 16; ++jj) L.ud[kk * 16 + jj] = u[jj];
           L.rp[k0 + kk] = rp;
           L.piv[k0 + kk] = piv;
         }
-      }
+      });
       if (bad && lane == 0) L.fail = 1;
     }
     GJ_STAMP(1);

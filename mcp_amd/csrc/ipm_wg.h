@@ -48,12 +48,16 @@ constexpr int kThreads = 256;       // workgroup size of every workgroup kernel 
 constexpr int kMaxDim = 768;        // largest system / vector dimension of the QP / affine kernels
 constexpr int kDimBuckets[4] = {128, 256, 512, 768};
 constexpr int kGjMax = 128;         // largest n of the QP family's workgroup SCHUR kernels (gj_vr.hpp)
-// doubles of the A block those kernels keep in LDS (m·n ≤ this): the largest m·n of bucket NV
-// (n ≤ 128, n + 2m ≤ NV), capped at 64 KB
+// The LDS row stride of that copy: odd, so the lanes' reads of one k over 16 rows (the
+// formation's A fragments, rr) fall in different banks (with m = 64 an even stride put all 16
+// rows in one bank).
+__host__ __device__ constexpr int kGjLda(int m) { return m | 1; }
+// doubles of the A block those kernels keep in LDS (n·kGjLda(m) ≤ this): the largest of bucket
+// NV (n ≤ 128, n + 2m ≤ NV), capped at 128 · 65 (KKT 256's n = 128, m = 64)
 constexpr int kGjACapOf(int nv) {
   int best = 1;
-  for (int n = 1; n <= kGjMax && n < nv; ++n) best = (n * ((nv - n) / 2) > best) ? n * ((nv - n) / 2) : best;
-  return best < 8192 ? best : 8192;
+  for (int n = 1; n <= kGjMax && n < nv; ++n) best = (n * kGjLda((nv - n) / 2) > best) ? n * kGjLda((nv - n) / 2) : best;
+  return best < 128 * 65 ? best : 128 * 65;
 }
 template <int NV>
 constexpr int kGjACap = kGjACapOf(NV);

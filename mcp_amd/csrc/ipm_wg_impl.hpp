@@ -609,9 +609,9 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
     // oracle's m_sym), else the pivoting LU at every step.  Once per instance.
     bool msym = false, a_lds = false;
     if constexpr (QPS) {
-      a_lds = n * m <= kGjACap<NVMAX>;
+      a_lds = n * kGjLda(m) <= kGjACap<NVMAX>;
       if (a_lds)
-        for (int q = tid; q < n * m; q += WG) sA[q] = th[(int64_t)n * n + q];
+        for (int q = tid; q < n * m; q += WG) sA[(q / m) * kGjLda(m) + q % m] = th[(int64_t)n * n + q];
       uint64_t asym = 0;
       for (int q = tid; q < n * n; q += WG) {
         const int j = q / n, i = q - j * n;
@@ -656,16 +656,17 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
             qt[k] = ry * Di;
           }
           __syncthreads();
-          auto rr = [&](const double* __restrict__ tA) {
+          // tA: row j of Aᵀ at tA[j·la] (θ: la = m; the LDS copy: kGjLda(m))
+          auto rr = [&](const double* __restrict__ tA, int la) {
             for (int i = tid; i < n; i += WG) {  // rr_i = −F_Gi + Σ_k A_ki ty_k
               double acc = -Fs[i];
-              for (int k = 0; k < m; ++k) acc = fma(tA[(int64_t)i * m + k], qt[k], acc);
+              for (int k = 0; k < m; ++k) acc = fma(tA[(int64_t)i * la + k], qt[k], acc);
               qr[i] = acc;
             }
           };
           for (int rep = 0; rep < (MCPX_WG_TWICE == 5 ? 2 : 1); ++rep) {
-            if (a_lds) rr(sA);
-            else rr(th + (int64_t)n * n);
+            if (a_lds) rr(sA, kGjLda(m));
+            else rr(th + (int64_t)n * n, m);
           }
           __syncthreads();
         } else if constexpr (SCH) {
@@ -761,8 +762,8 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
             for (int rep = 0; rep < (MCPX_WG_TWICE == 3 ? 2 : 1); ++rep) {
               d4 acc[GjDims<NSMAX>::TPW];
               for (int r2 = 0; r2 < (MCPX_WG_TWICE == 4 ? 2 : 1); ++r2) {
-                if (a_lds) gj_form<NSMAX>(acc, th, sA, n, m, tol, qd, qr);
-                else gj_form<NSMAX>(acc, th, th + (int64_t)n * n, n, m, tol, qd, qr);
+                if (a_lds) gj_form<NSMAX>(acc, th, sA, kGjLda(m), n, m, tol, qd, qr);
+                else gj_form<NSMAX>(acc, th, th + (int64_t)n * n, m, n, m, tol, qd, qr);
               }
               gj_ok = gj_solve<NSMAX>(acc, n, dzs, S.lu.gj);
             }
@@ -802,18 +803,18 @@ __device__ __forceinline__ void solve_instances(const WgArgs& W) {
           break;
         }
         if constexpr (QPS) {  // δy_k = (ry_k − Σ_j A_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
-          auto dyds = [&](const double* __restrict__ tA) {
+          auto dyds = [&](const double* __restrict__ tA, int la) {
             for (int k = tid; k < m; k += WG) {
               double acc = qy[k];
-              for (int j = 0; j < n; ++j) acc = fma(-tA[(int64_t)j * m + k], dzs[j], acc);
+              for (int j = 0; j < n; ++j) acc = fma(-tA[(int64_t)j * la + k], dzs[j], acc);
               const double dy = acc * qd[k];
               dzs[n + k] = dy;
               dzs[n + m + k] = fma(-zs[n + m + k], dy, -Fs[n + m + k]) * qw[k];
             }
           };
           for (int rep = 0; rep < (MCPX_WG_TWICE == 6 ? 2 : 1); ++rep) {
-            if (a_lds) dyds(sA);
-            else dyds(th + (int64_t)n * n);
+            if (a_lds) dyds(sA, kGjLda(m));
+            else dyds(th + (int64_t)n * n, m);
           }
         } else if constexpr (SCH) {  // δy_k = (ry_k − Σ_j R_kj δx_j)·D_k⁻¹, δs_k = (−F_Ck − s_k δy_k)·w_k⁻¹
           const int32_t* rp = GEN::rj_ptr();

@@ -81,6 +81,16 @@ int main(int argc, char** argv) {
     for (int w4 = 0; w4 < 4; ++w4)
       for (int i = 0; i < 16; ++i) tot[w4][i] += st[((size_t)b * 4 + w4) * 16 + i];
   for (int b = 0; b < B; ++b) { steps += nw[b]; solved += stv[b] == 0; }
+  // FNV-1a over x, y, s, kkt and the Newton counts: variants of the build must agree bit for bit
+  uint64_t dg = 1469598103934665603ull;
+  auto fold = [&](const void* dev, size_t bytes) {
+    std::vector<unsigned char> h(bytes);
+    (void)hipMemcpy(h.data(), dev, bytes, hipMemcpyDeviceToHost);
+    for (unsigned char c : h) dg = (dg ^ c) * 1099511628211ull;
+  };
+  fold(x, (size_t)B * n * 8); fold(y, (size_t)B * m * 8); fold(s, (size_t)B * m * 8); fold(kkt, (size_t)B * 8);
+  fold(newton, (size_t)B * 4);
+  printf("digest %016llx\n", (unsigned long long)dg);
   const char* nm[] = {"panel staging", "pivot block (1 wave)", "multipliers + pivot-row chains", "MFMA trailing update",
                       "solution", "formation of S", "", "", "wait after staging", "wait after pivot block",
                       "wait after multipliers/chains", "wait after trailing update"};
