@@ -47,6 +47,12 @@
 #ifndef MCPX_GJ_FORM_PAIR
 #define MCPX_GJ_FORM_PAIR 1
 #endif
+// MCPX_GJ_DPP_NOP: s_nop 1 ahead of each of the pivot block's DPP fmacs (0: the first of each
+// step only).  Their DPP source was last written a step earlier; tools/check_dpp_hazards.py
+// refuses a build in which the compiler placed a write of it right before.
+#ifndef MCPX_GJ_DPP_NOP
+#define MCPX_GJ_DPP_NOP 0
+#endif
 
 namespace mcpx {
 namespace wg {
@@ -86,16 +92,22 @@ __device__ __forceinline__ void gj_static_for(F&& f) {
 }
 
 // acc ← fma(nl, u, acc) with u = lane R of acc's 16-lane row (v_fmac_f64_dpp row_newbcast:R; the
-// DPP read precedes the write, so every lane sees lane R's old value).  s_nop 1: the two wait
-// states a VALU write needs before a DPP read of the same register, whatever the compiler
-// placed just ahead of the asm.
-#define GJ_FMAC_NB(R)                                                                                 \
-  case R:                                                                                             \
-    asm volatile("s_nop 1\n v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf" \
-                 : "+v"(acc)                                                                          \
-                 : "v"(nl));                                                                          \
+// DPP read precedes the write, so every lane sees lane R's old value).  PAD: s_nop 1 first — a
+// VALU write needs two wait states before a DPP read of its register, an EXEC write five before
+// any DPP instruction (the pivot block pads the first fmac of each step, which follows the
+// EXEC restore of the pivot lane's U stores; MCPX_GJ_DPP_NOP = 1 pads every one).
+#define GJ_FMAC_NB(R)                                                                                   \
+  case R:                                                                                               \
+    if (PAD)                                                                                            \
+      asm volatile("s_nop 1\n v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf" \
+                   : "+v"(acc)                                                                          \
+                   : "v"(nl));                                                                          \
+    else                                                                                                \
+      asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #R " row_mask:0xf bank_mask:0xf"           \
+                   : "+v"(acc)                                                                          \
+                   : "v"(nl));                                                                          \
     break;
-template <int R>
+template <int R, bool PAD>
 __device__ __forceinline__ void gj_fmac_bcast_self(double& acc, double nl) {
   switch (R) {
     GJ_FMAC_NB(0) GJ_FMAC_NB(1) GJ_FMAC_NB(2) GJ_FMAC_NB(3) GJ_FMAC_NB(4) GJ_FMAC_NB(5) GJ_FMAC_NB(6)
@@ -346,7 +358,10 @@ __device__ __forceinline__ bool gj_solve(d4 (&acc)[GjDims<NSMAX>::TPW], int n, d
         const double l = pr[kk] * rp;
         const double nl = me ? 0.0 : -l;
 #pragma unroll
-        for (int jj = kk + 1; jj < 16; ++jj) gj_fmac_bcast_self<kk>(pr[jj], nl);
+        for (int jj = kk + 1; jj < 16; ++jj) {
+          if (MCPX_GJ_DPP_NOP || jj == kk + 1) gj_fmac_bcast_self<kk, true>(pr[jj], nl);
+          else gj_fmac_bcast_self<kk, false>(pr[jj], nl);
+        }
         if (lane < 16) L.lb[lane * 16 + kk] = me ? 0.0 : l;  // (lanes kb … 15: rows beyond, never read)
         if (lane == 0) {
           L.rp[k0 + kk] = rp;
