@@ -134,14 +134,15 @@ def _indefinite(th, n, m, scale):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,B,case", [(128, 64, 48, "spd"), (100, 37, 32, "spd"), (70, 10, 32, "spd"),
                                         (33, 40, 32, "spd"), (128, 64, 8, "asym"), (60, 20, 16, "indef"),
-                                        (128, 64, 8, "sparse")])
+                                        (128, 64, 8, "sparse"), (100, 150, 16, "spd")])
 def test_qp_schur_workgroup_vs_oracle(gpu, oracle_lib, n, m, B, case):
     """The QP family's workgroup SCHUR step (csrc/gj_vr.hpp: the Schur complement on the matrix
     cores, blocked Gauss-Jordan with MFMA trailing updates) beyond the one-wave kernel's
     n + m ≤ 64: bit-exact against the oracle's SCHUR step (solve_one: S with the MFMA K padding,
     gj_spd_solve) — ragged n and m (panels and K-chunks not multiples of 16 / 4), M not symmetric
     (the pivoting LU at every step), M − c·I (pivots ≤ 0 on some steps: the LU fallback), sparse
-    QPs (failing instances, 931 Newton steps)."""
+    QPs (failing instances, 931 Newton steps); n = 100, m = 150 (bucket 512) reads A from θ, its
+    n·kGjLda(m) past the LDS copy's capacity."""
     from mcp_amd.batch import solve_batch
 
     sp = 0.9 if case == "sparse" else 0.0
